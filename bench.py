@@ -1,0 +1,242 @@
+#!/usr/bin/env python
+"""Benchmark: ViT-B/32 + LoRA r=8 encode of 224px images + 77-token captions
+(BASELINE.json configs[1]) on N GPUs, plus an optional cosine top-k search leg
+(configs[4] shape).
+
+  python bench.py [--gpus N] [--steps K] [--warmup W]
+  (N > 1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...)
+
+One step = every rank encodes its own batch (default 256 images + 256 captions,
+bf16 operands, LoRA merged) into L2-normalised fp32 embeddings; for N > 1 the
+step ends with the index-build exchange: an RCCL all-gather of every rank's
+embeddings over xGMI (scripts/rebuild_index.py builds the whole index), so per
+-GPU work is fixed as N grows ("weak" scaling). Inputs are resident in HBM
+before the timed region. Prints ONE JSON line on rank 0.
+
+value = image+text pairs encoded per second over all ranks.
+roofline = the MFMA GEMM kernel (dominant: ~97% of the step's FLOPs), timed
+live with HIP events on its launch stream in a separate profiled pass.
+cpu_baseline = transformers CLIPModel fp32 on the host cores (the arithmetic
+models/clip_model.py runs) with the restated PEFT LoRA, on a bounded sample.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+
+import clip_lora_match_amd as clm  # noqa: E402
+from clip_lora_match_amd import synthetic as syn  # noqa: E402
+from clip_lora_match_amd import weights as W  # noqa: E402
+from clip_lora_match_amd.engine import ClipLoraModel  # noqa: E402
+
+MFMA_PEAK_TFLOPS = 2500.0   # dense bf16/fp16 MFMA, MI355X (MI355X_MICROARCH.md chip table)
+HBM_PEAK_GBS = 8000.0
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def flops_per_pair(cfg) -> dict:
+    """Algorithmic FLOPs per image / caption (2 x MAC of every GEMM + full-T^2 attention,
+    LoRA unmerged), SURVEY §8(d)."""
+    def tower(d, L, mlp, T, lora_w):
+        per_layer = 2 * T * d * (3 * d + d + 2 * mlp) + 4 * T * T * d + lora_w * T
+        return L * per_layer
+    r = cfg.lora_r
+    lora_tok = lambda d: 2 * 4 * (2 * r * d)  # q,k,v,out: x.A^T (r x d) + (.)B^T (d x r)
+    v, t = cfg.vision, cfg.text
+    P = cfg.num_patches
+    img = tower(v.hidden, v.layers, v.mlp, P + 1, lora_tok(v.hidden)) \
+        + 2 * P * (cfg.channels * cfg.patch ** 2) * v.hidden + 2 * v.hidden * cfg.proj_dim
+    txt = tower(t.hidden, t.layers, t.mlp, cfg.max_pos, lora_tok(t.hidden)) + 2 * t.hidden * cfg.proj_dim
+    return {"image": float(img), "caption": float(txt)}
+
+
+def cpu_baseline(cfg, sd, lora, budget_s: float):
+    """transformers CLIPModel fp32 on the host cores + restated PEFT LoRA (oracle/hf_ref.py)."""
+    from oracle import hf_ref as H
+    cores = len(os.sched_getaffinity(0))
+    threads = max(1, min(cores, int(os.environ.get("OMP_NUM_THREADS", cores))))
+    torch.set_num_threads(threads)
+    m = H.hf_model(cfg, sd, lora)
+    n = 16
+    imgs = syn.images_u8(n, cfg.image_size, 777)
+    ids = syn.captions(n, cfg.max_pos, cfg.bos_token_id, cfg.eos_token_id, 778)
+    pv = H.pixel_values(cfg, imgs)
+    H.encode(m, cfg, pv[:2], ids[:2])  # warm
+    done, t0 = 0, time.perf_counter()
+    while True:
+        H.encode(m, cfg, pv, ids)
+        done += n
+        if time.perf_counter() - t0 > budget_s:
+            break
+    dt = time.perf_counter() - t0
+    # the reference's own call pattern: one image / one caption per call (clip_model.py:89-150)
+    t1 = time.perf_counter()
+    for i in range(4):
+        H.encode(m, cfg, pv[i:i + 1], ids[i:i + 1])
+    dt1 = time.perf_counter() - t1
+    return {"value": done / dt, "unit": "pairs/s", "cores": threads, "kind": "reference",
+            "sample": f"{done} image+caption pairs in batches of {n} ({dt:.1f} s), transformers "
+                      f"{__import__('transformers').__version__} CLIPModel fp32 + PEFT-equivalent LoRA hooks, "
+                      f"torch CPU {threads} threads; reference per-item loop (batch 1): {4 / dt1:.2f} pairs/s"}
+
+
+def search_leg(rows: int, queries: int, k: int, device):
+    from clip_lora_match_amd.search import CosineIndex
+    dim = 512
+    idx = CosineIndex(dim, capacity=rows, device=device)
+    g = torch.Generator(device=device).manual_seed(7)
+    chunk = 1 << 20
+    for r0 in range(0, rows, chunk):
+        n = min(chunk, rows - r0)
+        x = torch.randn((n, dim), generator=g, device=device)
+        idx.append((x / x.norm(dim=-1, keepdim=True)).half())
+        del x
+    q = torch.randn((queries, dim), generator=g, device=device)
+    q = (q / q.norm(dim=-1, keepdim=True)).half()
+    idx.search(q[:64], k)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    s, i = idx.search(q, k)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    idx.close()
+    flops = 2.0 * queries * rows * dim
+    return {"qps": queries / dt, "seconds": dt, "rows": rows, "queries": queries, "k": k, "dim": dim,
+            "index_dtype": "fp16", "tflops": flops / dt / 1e12}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=256)
+    ap.add_argument("--dtype", default="bfloat16", choices=["bfloat16", "float16"])
+    ap.add_argument("--lora-mode", default="merged", choices=["merged", "unmerged"])
+    ap.add_argument("--cpu-budget", type=float, default=12.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--search-rows", type=int, default=10_000_000)
+    ap.add_argument("--search-queries", type=int, default=10_000)
+    ap.add_argument("--no-search", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=dev)
+
+    cfg = clm.get_preset("ViT-B/32")   # LoRA r=8, alpha=16 on q,k,v,out (config/lora_config.yaml)
+    sd = W.synthetic_state_dict(cfg, 0)
+    lora = W.synthetic_lora(cfg, 1)
+    B = args.batch
+    model = ClipLoraModel(cfg, device=dev, compute_dtype=args.dtype, lora_mode=args.lora_mode, max_batch=B)
+    model.load_tensors(sd)
+    model.load_tensors(lora)
+    model.finalize()
+
+    imgs = torch.from_numpy(syn.images_u8(B, cfg.image_size, 1234 + rank * B)).to(dev)
+    ids = torch.from_numpy(syn.captions(B, cfg.max_pos, cfg.bos_token_id, cfg.eos_token_id, 99 + rank)).to(dev)
+    emb = torch.empty((2 * B, cfg.proj_dim), dtype=torch.float32, device=dev)
+    gathered = torch.empty((world * 2 * B, cfg.proj_dim), dtype=torch.float32, device=dev) if world > 1 else None
+
+    def step():
+        model.encode_pixels(imgs, out=emb[:B])
+        model.encode_ids(ids, out=emb[B:])
+        if world > 1:
+            torch.distributed.all_gather_into_tensor(gathered, emb)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([dt], dtype=torch.float64, device=dev)
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        dt = float(t.item())
+    ms_step = dt / args.steps * 1e3
+    pairs_s = world * B / (dt / args.steps)
+
+    # profiled pass (outside the timed region): HIP events around every kernel launch
+    model.prof_enable(True)
+    nprof = 3
+    for _ in range(nprof):
+        step()
+    torch.cuda.synchronize()
+    prof = model.prof_read()
+    model.prof_enable(False)
+    gemm_ms, gemm_flops, gemm_n = prof["gemm"]
+    fp = flops_per_pair(cfg)
+    step_flops = B * (fp["image"] + fp["caption"])
+
+    result = {
+        "metric": "image+text embeds/sec & cosine top-k QPS, ViT-B/32+LoRA, 1/2/4/8 MI355X",
+        "value": round(pairs_s, 1),
+        "unit": "image+text pairs/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_step, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "bf16" if args.dtype == "bfloat16" else "fp16",
+        "data": "synthetic (seeded uint8 224x224 RGB images, 77-token id captions; deterministic synthetic weights)",
+        "config": {"workload": "ViT-B/32 + LoRA r=8 alpha=16 (q,k,v,out, both towers) encode + L2-normalise",
+                   "per_gpu_batch": B, "global_batch": world * B, "seq_len": cfg.max_pos,
+                   "image_size": cfg.image_size, "lora_mode": args.lora_mode,
+                   "parallelism": f"dp{world}" + (" + all_gather(embeddings)" if world > 1 else "")},
+        "embeds_per_s": round(2 * pairs_s, 1),
+        "step_tflops_per_gpu": round(step_flops / (ms_step * 1e-3) / 1e12, 2),
+        "roofline": {
+            "kernel": "gemm_nt_kernel (MFMA 16x16x32, all encoder GEMMs)",
+            "bound": "mfma",
+            "achieved": round(gemm_flops / (gemm_ms * 1e-3) / 1e12, 2),
+            "peak": MFMA_PEAK_TFLOPS,
+            "unit": "TFLOP/s",
+            "frac": round(gemm_flops / (gemm_ms * 1e-3) / 1e12 / MFMA_PEAK_TFLOPS, 4),
+            "traffic": None,
+            "avg_launch_us": round(gemm_ms / gemm_n * 1e3, 2),
+            "launches_per_step": gemm_n // nprof,
+            "kernel_ms_per_step": {k: round(v[0] / nprof, 4) for k, v in prof.items()},
+        },
+    }
+    if rank == 0 and world == 1 and not args.no_search:
+        try:
+            result["search"] = search_leg(args.search_rows, args.search_queries, 5, dev)
+        except Exception as e:  # report, never hide
+            result["search"] = {"error": repr(e)}
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        result["cpu_baseline"] = cpu_baseline(cfg, sd, lora, args.cpu_budget)
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    model.close()
+    if world > 1:
+        torch.distributed.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

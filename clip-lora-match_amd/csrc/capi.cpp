@@ -1,0 +1,1066 @@
+// libclm C-ABI (include/clm.h): context, weight packing, encode drivers, HBM index.
+//
+// Host runtime behind the reference's Python API:
+//   load_clip_model            models/clip_model.py:37-82     -> clm_ctx_create/_load_tensor/_finalize
+//   PEFT LoRA (r, alpha/r)     models/lora_adapter.py:21-43    -> merged or K-extension packing
+//   encode_image/encode_text   models/clip_model.py:89-150     -> clm_encode_image/_text
+//   TextSearchIndex            src/embedding/search.py:24-115  -> clm_index_*
+// Weights arrive by transformers / PEFT state-dict name; finalize() fuses q/k/v
+// into one [3d, K] matrix (q rows pre-scaled by 64^-1/2), folds LoRA either into
+// the weights (W + (alpha/r) B A, fp32 then cast) or as K-extension columns
+// [W | (alpha/r) B] against activations [X | X A^T], and uploads everything in
+// the compute dtype (bf16/fp16), keeping LayerNorm, biases, embeddings and the
+// projections in fp32.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "clm.h"
+#include "kernels.hpp"
+
+using namespace clm;
+
+namespace {
+
+thread_local std::string g_err;
+int fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+#define HIPCHK(x)                                                                              \
+  do {                                                                                         \
+    hipError_t e_ = (x);                                                                       \
+    if (e_ != hipSuccess) return fail(CLM_E_HIP, std::string(#x) + ": " + hipGetErrorString(e_)); \
+  } while (0)
+
+struct DeviceGuard {
+  int prev = -1;
+  explicit DeviceGuard(int dev) {
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    if (prev != dev) (void)hipSetDevice(dev);
+  }
+  ~DeviceGuard() {
+    int cur = -1;
+    if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+  }
+};
+
+bool is_device_ptr(const void* p) {
+  if (!p) return false;
+  hipPointerAttribute_t a;
+  if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+    (void)hipGetLastError();
+    return false;
+  }
+  return a.type == hipMemoryTypeDevice;
+}
+
+uint16_t host_f32_to_bf16(float f) {
+  uint32_t u;
+  std::memcpy(&u, &f, 4);
+  if ((u & 0x7fffffffu) > 0x7f800000u) return (uint16_t)((u >> 16) | 0x40);
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return (uint16_t)(u >> 16);
+}
+uint16_t host_f32_to_f16(float f) {
+  _Float16 h = (_Float16)f;
+  uint16_t r;
+  std::memcpy(&r, &h, 2);
+  return r;
+}
+float host_f16_to_f32(uint16_t v) {
+  _Float16 h;
+  std::memcpy(&h, &v, 2);
+  return (float)h;
+}
+float host_bf16_to_f32(uint16_t v) {
+  uint32_t u = (uint32_t)v << 16;
+  float f;
+  std::memcpy(&f, &u, 4);
+  return f;
+}
+
+int64_t round_up(int64_t x, int64_t m) { return (x + m - 1) / m * m; }
+
+struct HostTensor {
+  std::vector<int64_t> shape;
+  std::vector<float> data;
+};
+
+struct LayerW {
+  float *ln1_g = nullptr, *ln1_b = nullptr, *ln2_g = nullptr, *ln2_b = nullptr;
+  u16* w_qkv = nullptr; float* b_qkv = nullptr; int k_qkv = 0;
+  u16* w_out = nullptr; float* b_out = nullptr; int k_out = 0;
+  u16* w_fc1 = nullptr; float* b_fc1 = nullptr; int k_fc1 = 0;
+  u16* w_fc2 = nullptr; float* b_fc2 = nullptr; int k_fc2 = 0;
+  float* a_qkv = nullptr; int r_qkv = 0;   // unmerged LoRA A (fp32) per GEMM input
+  float* a_out = nullptr; int r_out = 0;
+  float* a_fc1 = nullptr; int r_fc1 = 0;
+  float* a_fc2 = nullptr; int r_fc2 = 0;
+};
+
+struct Tower {
+  bool vision = false;
+  int d = 0, L = 0, H = 0, mlp = 0;
+  std::vector<LayerW> layers;
+  float *projT = nullptr, *fin_g = nullptr, *fin_b = nullptr;
+  // vision
+  u16* patch_w = nullptr; int kp = 0;
+  float *cls = nullptr, *pos = nullptr, *pre_g = nullptr, *pre_b = nullptr, *lut = nullptr;
+  // text
+  float *tok = nullptr, *tpos = nullptr;
+  // workspace
+  int64_t maxM = 0;
+  float* h = nullptr;
+  u16 *X = nullptr, *QKV = nullptr, *O = nullptr, *Hm = nullptr, *P = nullptr;
+  int64_t ldx = 0, ldo = 0, ldm = 0;
+};
+
+constexpr int RPAD = 64;  // K-extension width of the unmerged LoRA mode (K stays a multiple of 64)
+
+}  // namespace
+
+struct clm_ctx {
+  int dev = 0;
+  clm_model_desc desc{};
+  bool finalized = false;
+  bool lora_enabled = true;
+  std::unordered_map<std::string, HostTensor> host;
+  std::vector<void*> allocs;       // weights + workspace
+  Tower vis, txt;
+  // host<->device staging
+  void* stage_in = nullptr; size_t stage_in_bytes = 0;
+  void* stage_out = nullptr; size_t stage_out_bytes = 0;
+  int32_t* ids_dev = nullptr;
+  // kernel timing (clm_prof_*): events recorded on the launch stream
+  bool prof = false;
+  std::vector<hipEvent_t> ev_pool;
+  size_t ev_used = 0;
+  struct Rec { int cat; double work; size_t e0, e1; };
+  std::vector<Rec> recs;
+
+  bool bf16() const { return desc.compute_dtype == CLM_BF16; }
+
+  template <typename T>
+  int dalloc(T** p, size_t count) {
+    void* q = nullptr;
+    if (count == 0) count = 1;
+    if (hipMalloc(&q, count * sizeof(T)) != hipSuccess) {
+      (void)hipGetLastError();
+      return fail(CLM_E_OOM, "hipMalloc of " + std::to_string(count * sizeof(T)) + " bytes failed");
+    }
+    allocs.push_back(q);
+    *p = (T*)q;
+    return CLM_OK;
+  }
+  void free_all() {
+    for (void* p : allocs) (void)hipFree(p);
+    allocs.clear();
+    if (stage_in) (void)hipFree(stage_in);
+    if (stage_out) (void)hipFree(stage_out);
+    stage_in = stage_out = nullptr;
+    stage_in_bytes = stage_out_bytes = 0;
+    vis = Tower();
+    txt = Tower();
+    ids_dev = nullptr;
+  }
+};
+
+struct clm_index {
+  int dev = 0;
+  int64_t cap = 0, n = 0, dim = 0, offset = 0;
+  u16* rows = nullptr;
+  float* inv = nullptr;
+  // search workspace (grown on demand)
+  void* ws = nullptr; size_t ws_bytes = 0;
+};
+
+namespace {
+
+const HostTensor* find(const clm_ctx* c, const std::string& n) {
+  auto it = c->host.find(n);
+  return it == c->host.end() ? nullptr : &it->second;
+}
+
+int need(const clm_ctx* c, const std::string& n, int64_t numel, const HostTensor** out) {
+  const HostTensor* t = find(c, n);
+  if (!t) return fail(CLM_E_MISSING, "missing tensor '" + n + "'");
+  if ((int64_t)t->data.size() != numel)
+    return fail(CLM_E_ARG, "tensor '" + n + "' has " + std::to_string(t->data.size()) + " elements, expected " +
+                               std::to_string(numel));
+  *out = t;
+  return CLM_OK;
+}
+
+int upload_f32(clm_ctx* c, const std::vector<float>& v, float** dst) {
+  int r = c->dalloc(dst, v.size());
+  if (r) return r;
+  HIPCHK(hipMemcpy(*dst, v.data(), v.size() * sizeof(float), hipMemcpyHostToDevice));
+  return CLM_OK;
+}
+
+int upload_16(clm_ctx* c, const std::vector<float>& v, u16** dst) {
+  std::vector<u16> h(v.size());
+  if (c->bf16())
+    for (size_t i = 0; i < v.size(); ++i) h[i] = host_f32_to_bf16(v[i]);
+  else
+    for (size_t i = 0; i < v.size(); ++i) h[i] = host_f32_to_f16(v[i]);
+  int r = c->dalloc(dst, h.size());
+  if (r) return r;
+  HIPCHK(hipMemcpy(*dst, h.data(), h.size() * sizeof(u16), hipMemcpyHostToDevice));
+  return CLM_OK;
+}
+
+int get_f32(clm_ctx* c, const std::string& n, int64_t numel, float** dst) {
+  const HostTensor* t;
+  int r = need(c, n, numel, &t);
+  if (r) return r;
+  return upload_f32(c, t->data, dst);
+}
+
+// A linear's weight block for a (possibly fused) GEMM: rows [row0, row0+out) of W,
+// its LoRA pair (if targeted and enabled), and the extension offset for unmerged mode.
+struct LinearSpec {
+  std::string path;
+  int in, out;
+  bool lora;
+};
+
+// Build a fused [sum(out), K] weight (fp32 host) for linears sharing one input.
+// merged: W += s * B A.  unmerged: K = in + RPAD, columns [in + off, in + off + r) = s * B.
+// Also returns the stacked A [r_ext, in] for the unmerged mode.
+int build_fused(clm_ctx* c, const std::vector<LinearSpec>& specs, bool q_scale_first, std::vector<float>& W,
+                std::vector<float>& bias, int& K, std::vector<float>& A_stack, int& r_ext) {
+  const clm_model_desc& d = c->desc;
+  const bool unmerged = d.lora_mode == CLM_LORA_UNMERGED;
+  const int in = specs[0].in;
+  int total_out = 0;
+  r_ext = 0;
+  for (auto& s : specs) {
+    total_out += s.out;
+    if (s.lora) r_ext += d.lora_r;
+  }
+  K = (unmerged && r_ext > 0) ? in + RPAD : in;
+  if (r_ext > RPAD) return fail(CLM_E_ARG, "LoRA rank too large for the K-extension (sum r > 64)");
+  W.assign((size_t)total_out * K, 0.f);
+  bias.assign(total_out, 0.f);
+  A_stack.assign((size_t)r_ext * in, 0.f);
+  const float scaling = d.lora_r > 0 ? d.lora_alpha / (float)d.lora_r : 0.f;
+  int row0 = 0, roff = 0;
+  for (size_t si = 0; si < specs.size(); ++si) {
+    const LinearSpec& s = specs[si];
+    const HostTensor *w, *b;
+    int r = need(c, s.path + ".weight", (int64_t)s.out * s.in, &w);
+    if (r) return r;
+    r = need(c, s.path + ".bias", s.out, &b);
+    if (r) return r;
+    const float qs = (q_scale_first && si == 0) ? 0.125f : 1.0f;  // head_dim 64 -> 64^-1/2
+    for (int o = 0; o < s.out; ++o) {
+      std::memcpy(&W[(size_t)(row0 + o) * K], &w->data[(size_t)o * s.in], s.in * sizeof(float));
+      bias[row0 + o] = b->data[o];
+    }
+    if (s.lora) {
+      const HostTensor *A, *B;
+      const std::string base = "base_model.model." + s.path;
+      r = need(c, base + ".lora_A.weight", (int64_t)d.lora_r * s.in, &A);
+      if (r) return r;
+      r = need(c, base + ".lora_B.weight", (int64_t)s.out * d.lora_r, &B);
+      if (r) return r;
+      if (!unmerged) {
+        for (int o = 0; o < s.out; ++o) {
+          float* wr = &W[(size_t)(row0 + o) * K];
+          for (int j = 0; j < d.lora_r; ++j) {
+            const float bj = scaling * B->data[(size_t)o * d.lora_r + j];
+            const float* ar = &A->data[(size_t)j * s.in];
+            for (int i = 0; i < s.in; ++i) wr[i] += bj * ar[i];
+          }
+        }
+      } else {
+        for (int o = 0; o < s.out; ++o)
+          for (int j = 0; j < d.lora_r; ++j)
+            W[(size_t)(row0 + o) * K + s.in + roff + j] = scaling * B->data[(size_t)o * d.lora_r + j];
+        std::memcpy(&A_stack[(size_t)roff * in], A->data.data(), (size_t)d.lora_r * in * sizeof(float));
+      }
+      roff += d.lora_r;
+    }
+    if (qs != 1.0f) {
+      for (int o = 0; o < s.out; ++o) {
+        float* wr = &W[(size_t)(row0 + o) * K];
+        for (int i = 0; i < K; ++i) wr[i] *= qs;
+        bias[row0 + o] *= qs;
+      }
+    }
+    row0 += s.out;
+  }
+  if (!unmerged) r_ext = 0;
+  return CLM_OK;
+}
+
+int build_tower(clm_ctx* c, Tower& T, bool vision) {
+  const clm_model_desc& d = c->desc;
+  const clm_tower_desc& td = vision ? d.vision : d.text;
+  T.vision = vision;
+  T.d = td.hidden; T.L = td.layers; T.H = td.heads; T.mlp = td.mlp;
+  if (T.d != T.H * 64) return fail(CLM_E_ARG, "head_dim must be 64");
+  if (T.d % 128 || T.d > 1024 || T.mlp % 64) return fail(CLM_E_ARG, "hidden must be a multiple of 128 (<=1024), mlp of 64");
+  const std::string pre = vision ? "vision_model" : "text_model";
+  const bool lora_on = c->lora_enabled && d.lora_r > 0;
+  const uint32_t tg = lora_on ? d.lora_targets : 0u;
+  const bool unmerged = d.lora_mode == CLM_LORA_UNMERGED;
+  int r;
+  T.layers.resize(T.L);
+  for (int l = 0; l < T.L; ++l) {
+    LayerW& Lw = T.layers[l];
+    const std::string p = pre + ".encoder.layers." + std::to_string(l);
+    if ((r = get_f32(c, p + ".layer_norm1.weight", T.d, &Lw.ln1_g))) return r;
+    if ((r = get_f32(c, p + ".layer_norm1.bias", T.d, &Lw.ln1_b))) return r;
+    if ((r = get_f32(c, p + ".layer_norm2.weight", T.d, &Lw.ln2_g))) return r;
+    if ((r = get_f32(c, p + ".layer_norm2.bias", T.d, &Lw.ln2_b))) return r;
+    std::vector<float> W, b, A;
+    int K, rext;
+    // q, k, v share the LN1 output: one fused GEMM
+    std::vector<LinearSpec> qkv = {{p + ".self_attn.q_proj", T.d, T.d, (tg & CLM_LORA_Q) != 0},
+                                   {p + ".self_attn.k_proj", T.d, T.d, (tg & CLM_LORA_K) != 0},
+                                   {p + ".self_attn.v_proj", T.d, T.d, (tg & CLM_LORA_V) != 0}};
+    if ((r = build_fused(c, qkv, true, W, b, K, A, rext))) return r;
+    if ((r = upload_16(c, W, &Lw.w_qkv)) || (r = upload_f32(c, b, &Lw.b_qkv))) return r;
+    Lw.k_qkv = K; Lw.r_qkv = rext;
+    if (unmerged && rext && (r = upload_f32(c, A, &Lw.a_qkv))) return r;
+
+    std::vector<LinearSpec> outp = {{p + ".self_attn.out_proj", T.d, T.d, (tg & CLM_LORA_OUT) != 0}};
+    if ((r = build_fused(c, outp, false, W, b, K, A, rext))) return r;
+    if ((r = upload_16(c, W, &Lw.w_out)) || (r = upload_f32(c, b, &Lw.b_out))) return r;
+    Lw.k_out = K; Lw.r_out = rext;
+    if (unmerged && rext && (r = upload_f32(c, A, &Lw.a_out))) return r;
+
+    std::vector<LinearSpec> fc1 = {{p + ".mlp.fc1", T.d, T.mlp, (tg & CLM_LORA_FC1) != 0}};
+    if ((r = build_fused(c, fc1, false, W, b, K, A, rext))) return r;
+    if ((r = upload_16(c, W, &Lw.w_fc1)) || (r = upload_f32(c, b, &Lw.b_fc1))) return r;
+    Lw.k_fc1 = K; Lw.r_fc1 = rext;
+    if (unmerged && rext && (r = upload_f32(c, A, &Lw.a_fc1))) return r;
+
+    std::vector<LinearSpec> fc2 = {{p + ".mlp.fc2", T.mlp, T.d, (tg & CLM_LORA_FC2) != 0}};
+    if ((r = build_fused(c, fc2, false, W, b, K, A, rext))) return r;
+    if ((r = upload_16(c, W, &Lw.w_fc2)) || (r = upload_f32(c, b, &Lw.b_fc2))) return r;
+    Lw.k_fc2 = K; Lw.r_fc2 = rext;
+    if (unmerged && rext && (r = upload_f32(c, A, &Lw.a_fc2))) return r;
+  }
+  // projection, transposed to [d, D] for coalesced reads in pool_project
+  {
+    const HostTensor* pw;
+    const std::string pn = vision ? "visual_projection.weight" : "text_projection.weight";
+    if ((r = need(c, pn, (int64_t)d.proj_dim * T.d, &pw))) return r;
+    std::vector<float> pt((size_t)T.d * d.proj_dim);
+    for (int j = 0; j < d.proj_dim; ++j)
+      for (int i = 0; i < T.d; ++i) pt[(size_t)i * d.proj_dim + j] = pw->data[(size_t)j * T.d + i];
+    if ((r = upload_f32(c, pt, &T.projT))) return r;
+  }
+  const int64_t B = d.max_batch;
+  if (vision) {
+    const int G = d.image_size / d.patch, Tn = G * G + 1;
+    if ((r = get_f32(c, pre + ".post_layernorm.weight", T.d, &T.fin_g))) return r;
+    if ((r = get_f32(c, pre + ".post_layernorm.bias", T.d, &T.fin_b))) return r;
+    if ((r = get_f32(c, pre + ".pre_layrnorm.weight", T.d, &T.pre_g))) return r;
+    if ((r = get_f32(c, pre + ".pre_layrnorm.bias", T.d, &T.pre_b))) return r;
+    if ((r = get_f32(c, pre + ".embeddings.class_embedding", T.d, &T.cls))) return r;
+    if ((r = get_f32(c, pre + ".embeddings.position_embedding.weight", (int64_t)Tn * T.d, &T.pos))) return r;
+    const int kreal = d.channels * d.patch * d.patch;
+    T.kp = (int)round_up(kreal, 64);
+    const HostTensor* pw;
+    if ((r = need(c, pre + ".embeddings.patch_embedding.weight", (int64_t)T.d * kreal, &pw))) return r;
+    std::vector<float> wp((size_t)T.d * T.kp, 0.f);
+    for (int o = 0; o < T.d; ++o) std::memcpy(&wp[(size_t)o * T.kp], &pw->data[(size_t)o * kreal], kreal * 4);
+    if ((r = upload_16(c, wp, &T.patch_w))) return r;
+    // CLIPImageProcessor rescale (float64 multiply -> float32) then (x - mean) / std in float32
+    std::vector<float> lut((size_t)d.channels * 256);
+    for (int ch = 0; ch < d.channels; ++ch)
+      for (int u = 0; u < 256; ++u) {
+        const float x = (float)((double)u * (1.0 / 255.0));
+        lut[(size_t)ch * 256 + u] = (x - d.mean[ch % 3]) / d.std[ch % 3];
+      }
+    if ((r = upload_f32(c, lut, &T.lut))) return r;
+    T.maxM = B * Tn;
+    if ((r = c->dalloc(&T.P, (size_t)B * G * G * T.kp))) return r;
+  } else {
+    if ((r = get_f32(c, pre + ".final_layer_norm.weight", T.d, &T.fin_g))) return r;
+    if ((r = get_f32(c, pre + ".final_layer_norm.bias", T.d, &T.fin_b))) return r;
+    if ((r = get_f32(c, pre + ".embeddings.token_embedding.weight", (int64_t)d.vocab * T.d, &T.tok))) return r;
+    if ((r = get_f32(c, pre + ".embeddings.position_embedding.weight", (int64_t)d.max_pos * T.d, &T.tpos))) return r;
+    T.maxM = B * d.max_pos;
+  }
+  T.ldx = T.d + RPAD;
+  T.ldo = T.d + RPAD;
+  T.ldm = T.mlp + RPAD;
+  if ((r = c->dalloc(&T.h, (size_t)T.maxM * T.d))) return r;
+  if ((r = c->dalloc(&T.X, (size_t)T.maxM * T.ldx))) return r;
+  if ((r = c->dalloc(&T.QKV, (size_t)T.maxM * 3 * T.d))) return r;
+  if ((r = c->dalloc(&T.O, (size_t)T.maxM * T.ldo))) return r;
+  if ((r = c->dalloc(&T.Hm, (size_t)T.maxM * T.ldm))) return r;
+  return CLM_OK;
+}
+
+int ensure_stage(void** p, size_t* cap, size_t bytes) {
+  if (*cap >= bytes) return CLM_OK;
+  if (*p) (void)hipFree(*p);
+  *p = nullptr;
+  *cap = 0;
+  if (hipMalloc(p, bytes) != hipSuccess) {
+    (void)hipGetLastError();
+    *p = nullptr;
+    return fail(CLM_E_OOM, "staging allocation failed");
+  }
+  *cap = bytes;
+  return CLM_OK;
+}
+
+// time one launch when profiling is on: returns the event-pair slot or -1
+struct ProfScope {
+  clm_ctx* c; hipStream_t st; int cat; double work; size_t e0 = 0; bool on = false;
+  ProfScope(clm_ctx* c_, hipStream_t st_, int cat_, double work_) : c(c_), st(st_), cat(cat_), work(work_) {
+    if (!c->prof) return;
+    if (c->ev_used + 2 > c->ev_pool.size()) {
+      for (int i = 0; i < 256; ++i) {
+        hipEvent_t e;
+        if (hipEventCreate(&e) != hipSuccess) { (void)hipGetLastError(); return; }
+        c->ev_pool.push_back(e);
+      }
+    }
+    e0 = c->ev_used;
+    c->ev_used += 2;
+    on = hipEventRecord(c->ev_pool[e0], st) == hipSuccess;
+  }
+  ~ProfScope() {
+    if (!on) return;
+    if (hipEventRecord(c->ev_pool[e0 + 1], st) == hipSuccess) c->recs.push_back({cat, work, e0, e0 + 1});
+  }
+};
+#define PROF(cat, work) ProfScope prof_scope_##__LINE__(c, st, cat, work)
+
+#define KCHK(x)                                                                                   \
+  do {                                                                                            \
+    hipError_t e_ = (x);                                                                          \
+    if (e_ != hipSuccess) return fail(CLM_E_HIP, std::string("kernel launch ") + #x + ": " + hipGetErrorString(e_)); \
+  } while (0)
+
+// LN into X for a layer's q/k/v GEMM input (A_qkv extension in unmerged mode)
+LnArgs ln_into_x(clm_ctx* c, Tower& T, int64_t M, const float* g, const float* b, const float* loraA, int r_ext) {
+  LnArgs a{};
+  a.mode = 0; a.src = T.h; a.lds = T.d; a.hf = T.h; a.ldh = T.d;
+  a.g1 = g; a.b1 = b; a.y = T.X; a.ldy = T.ldx;
+  a.loraA = loraA; a.r_ext = r_ext; a.r_pad = loraA ? RPAD : 0;
+  a.M = (int)M; a.d = T.d; a.eps = c->desc.ln_eps;
+  return a;
+}
+
+// encoder layers on the residual stream T.h; the first layer's LN1 output must already be in T.X
+int run_layers(clm_ctx* c, Tower& T, int B, int S, bool causal, hipStream_t st) {
+  const bool bf = c->bf16();
+  const int64_t M = (int64_t)B * S;
+  for (int l = 0; l < T.L; ++l) {
+    LayerW& Lw = T.layers[l];
+    GemmArgs g{};
+    g.A = T.X; g.lda = T.ldx; g.W = Lw.w_qkv; g.ldw = Lw.k_qkv; g.M = (int)M; g.N = 3 * T.d; g.K = Lw.k_qkv;
+    g.out = T.QKV; g.ldo = 3 * T.d; g.bias = Lw.b_qkv;
+    { PROF(CLM_PROF_GEMM, 2.0 * M * g.N * g.K); KCHK(gemm(bf, EPI_STORE, g, st)); }
+    { PROF(CLM_PROF_ATTN, 4.0 * B * T.H * (double)S * S * 64);
+      KCHK(attention(bf, causal, T.QKV, 3 * T.d, T.O, T.ldo, B, S, T.H, T.d, st)); }
+    if (Lw.r_out) { PROF(CLM_PROF_OTHER, 2.0 * M * T.d + 4.0 * Lw.r_out * T.d);
+      KCHK(lora_down(bf, T.O, T.ldo, (int)M, T.d, Lw.a_out, Lw.r_out, RPAD, st)); }
+    g = GemmArgs{};
+    g.A = T.O; g.lda = T.ldo; g.W = Lw.w_out; g.ldw = Lw.k_out; g.M = (int)M; g.N = T.d; g.K = Lw.k_out;
+    g.out = T.h; g.ldo = T.d; g.bias = Lw.b_out;
+    { PROF(CLM_PROF_GEMM, 2.0 * M * g.N * g.K); KCHK(gemm(bf, EPI_RESID, g, st)); }
+    { PROF(CLM_PROF_LN, (double)M * T.d * 6.0);
+      KCHK(layernorm(bf, ln_into_x(c, T, M, Lw.ln2_g, Lw.ln2_b, Lw.a_fc1, Lw.r_fc1), st)); }
+    g = GemmArgs{};
+    g.A = T.X; g.lda = T.ldx; g.W = Lw.w_fc1; g.ldw = Lw.k_fc1; g.M = (int)M; g.N = T.mlp; g.K = Lw.k_fc1;
+    g.out = T.Hm; g.ldo = T.ldm; g.bias = Lw.b_fc1;
+    { PROF(CLM_PROF_GEMM, 2.0 * M * g.N * g.K); KCHK(gemm(bf, EPI_GELU, g, st)); }
+    if (Lw.r_fc2) { PROF(CLM_PROF_OTHER, 2.0 * M * T.mlp + 4.0 * Lw.r_fc2 * T.mlp);
+      KCHK(lora_down(bf, T.Hm, T.ldm, (int)M, T.mlp, Lw.a_fc2, Lw.r_fc2, RPAD, st)); }
+    g = GemmArgs{};
+    g.A = T.Hm; g.lda = T.ldm; g.W = Lw.w_fc2; g.ldw = Lw.k_fc2; g.M = (int)M; g.N = T.d; g.K = Lw.k_fc2;
+    g.out = T.h; g.ldo = T.d; g.bias = Lw.b_fc2;
+    { PROF(CLM_PROF_GEMM, 2.0 * M * g.N * g.K); KCHK(gemm(bf, EPI_RESID, g, st)); }
+    if (l + 1 < T.L) {
+      LayerW& Ln = T.layers[l + 1];
+      PROF(CLM_PROF_LN, (double)M * T.d * 6.0);
+      KCHK(layernorm(bf, ln_into_x(c, T, M, Ln.ln1_g, Ln.ln1_b, Ln.a_qkv, Ln.r_qkv), st));
+    }
+  }
+  return CLM_OK;
+}
+
+int encode_image_chunk(clm_ctx* c, const void* pix, int layout, int B, void* out, int out_dtype, int normalize,
+                       hipStream_t st) {
+  const clm_model_desc& d = c->desc;
+  Tower& T = c->vis;
+  const bool bf = c->bf16();
+  const int G = d.image_size / d.patch, Tn = G * G + 1;
+  { PROF(CLM_PROF_OTHER, (double)B * G * G * T.kp * 2.0 + (double)B * d.image_size * d.image_size * d.channels);
+    KCHK(patchify(bf, pix, layout, B, d.image_size, d.patch, d.channels, T.lut, T.P, T.kp, st)); }
+  GemmArgs g{};
+  g.A = T.P; g.lda = T.kp; g.W = T.patch_w; g.ldw = T.kp; g.M = B * G * G; g.N = T.d; g.K = T.kp;
+  g.out = T.h; g.ldo = T.d; g.aux = T.pos; g.aux_ld = T.d; g.group = G * G;
+  { PROF(CLM_PROF_GEMM, 2.0 * g.M * g.N * g.K); KCHK(gemm(bf, EPI_PATCH, g, st)); }
+  { PROF(CLM_PROF_OTHER, (double)B * T.d * 4.0); KCHK(write_cls(T.h, T.d, B, Tn, T.d, T.cls, T.pos, st)); }
+  LnArgs a = ln_into_x(c, T, (int64_t)B * Tn, T.pre_g, T.pre_b, T.layers[0].a_qkv, T.layers[0].r_qkv);
+  a.g2 = T.layers[0].ln1_g; a.b2 = T.layers[0].ln1_b;  // pre_layrnorm (in place) then layer-0 LN1
+  { PROF(CLM_PROF_LN, (double)B * Tn * T.d * 10.0); KCHK(layernorm(bf, a, st)); }
+  int r = run_layers(c, T, B, Tn, false, st);
+  if (r) return r;
+  { PROF(CLM_PROF_OTHER, (double)B * (T.d * 4.0 + d.proj_dim * 4.0) + (double)T.d * d.proj_dim * 4.0);
+    KCHK(pool_project(T.h, T.d, B, Tn, T.d, nullptr, d.eos_token_id, T.fin_g, T.fin_b, d.ln_eps, T.projT,
+                      d.proj_dim, out, out_dtype == CLM_F32 ? 0 : 1, normalize, st)); }
+  return CLM_OK;
+}
+
+int encode_text_chunk(clm_ctx* c, const int32_t* ids_dev, int B, int L, void* out, int out_dtype, int normalize,
+                      hipStream_t st) {
+  const clm_model_desc& d = c->desc;
+  Tower& T = c->txt;
+  const bool bf = c->bf16();
+  LnArgs a{};
+  a.mode = 1; a.ids = ids_dev; a.tok = T.tok; a.pos = T.tpos; a.L = L;
+  a.hf = T.h; a.ldh = T.d; a.g1 = T.layers[0].ln1_g; a.b1 = T.layers[0].ln1_b;
+  a.y = T.X; a.ldy = T.ldx; a.loraA = T.layers[0].a_qkv; a.r_ext = T.layers[0].r_qkv;
+  a.r_pad = a.loraA ? RPAD : 0; a.M = B * L; a.d = T.d; a.eps = d.ln_eps;
+  { PROF(CLM_PROF_LN, (double)B * L * T.d * 14.0); KCHK(layernorm(bf, a, st)); }
+  int r = run_layers(c, T, B, L, true, st);
+  if (r) return r;
+  { PROF(CLM_PROF_OTHER, (double)B * (T.d * 4.0 + d.proj_dim * 4.0 + L * 4.0) + (double)T.d * d.proj_dim * 4.0);
+    KCHK(pool_project(T.h, T.d, B, L, T.d, ids_dev, d.eos_token_id, T.fin_g, T.fin_b, d.ln_eps, T.projT,
+                      d.proj_dim, out, out_dtype == CLM_F32 ? 0 : 1, normalize, st)); }
+  return CLM_OK;
+}
+
+size_t dtype_size(int dt) {
+  switch (dt) {
+    case CLM_F32: case CLM_I32: return 4;
+    case CLM_F16: case CLM_BF16: return 2;
+    case CLM_U8: return 1;
+    case CLM_I64: return 8;
+  }
+  return 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* clm_last_error(void) { return g_err.c_str(); }
+const char* clm_version(void) { return "clm 0.1.0 gfx950"; }
+int32_t clm_model_desc_size(void) { return (int32_t)sizeof(clm_model_desc); }
+
+int clm_prof_enable(clm_ctx* ctx, int enable) {
+  if (!ctx) return fail(CLM_E_ARG, "null ctx");
+  DeviceGuard g(ctx->dev);
+  (void)hipDeviceSynchronize();
+  ctx->prof = enable != 0;
+  ctx->recs.clear();
+  ctx->ev_used = 0;
+  return CLM_OK;
+}
+
+int clm_prof_read(clm_ctx* ctx, int category, double* ms, double* work, int64_t* launches) {
+  if (!ctx || category < 0 || category >= CLM_PROF_NCAT) return fail(CLM_E_ARG, "bad argument");
+  DeviceGuard g(ctx->dev);
+  double t = 0, w = 0;
+  int64_t n = 0;
+  for (auto& r : ctx->recs) {
+    if (r.cat != category) continue;
+    HIPCHK(hipEventSynchronize(ctx->ev_pool[r.e1]));
+    float m = 0.f;
+    HIPCHK(hipEventElapsedTime(&m, ctx->ev_pool[r.e0], ctx->ev_pool[r.e1]));
+    t += m; w += r.work; ++n;
+  }
+  if (ms) *ms = t;
+  if (work) *work = w;
+  if (launches) *launches = n;
+  return CLM_OK;
+}
+
+int clm_ctx_create(int hip_device, const clm_model_desc* desc, clm_ctx** out) {
+  if (!desc || !out) return fail(CLM_E_ARG, "null argument");
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) {
+    (void)hipGetLastError();
+    return fail(CLM_E_HIP, "no HIP device available");
+  }
+  if (hip_device < 0 || hip_device >= ndev) return fail(CLM_E_ARG, "bad device index");
+  if (desc->compute_dtype != CLM_BF16 && desc->compute_dtype != CLM_F16)
+    return fail(CLM_E_ARG, "compute_dtype must be CLM_BF16 or CLM_F16");
+  if (desc->max_batch <= 0 || desc->patch <= 0 || desc->image_size % desc->patch)
+    return fail(CLM_E_ARG, "bad max_batch / patch / image_size");
+  if (desc->max_pos > 77 * 4 || desc->proj_dim > 1024) return fail(CLM_E_ARG, "bad max_pos / proj_dim");
+  if (desc->lora_r < 0 || desc->lora_r > 64) return fail(CLM_E_ARG, "lora_r must be in [0, 64]");
+  clm_ctx* c = new clm_ctx();
+  c->dev = hip_device;
+  c->desc = *desc;
+  *out = c;
+  return CLM_OK;
+}
+
+int clm_ctx_destroy(clm_ctx* ctx) {
+  if (!ctx) return CLM_OK;
+  DeviceGuard g(ctx->dev);
+  (void)hipDeviceSynchronize();
+  ctx->free_all();
+  for (hipEvent_t e : ctx->ev_pool) (void)hipEventDestroy(e);
+  delete ctx;
+  return CLM_OK;
+}
+
+int clm_load_tensor(clm_ctx* ctx, const char* name, const void* host_ptr, int dtype, const int64_t* shape,
+                    int ndim) {
+  if (!ctx || !name || (!host_ptr && ndim > 0) || ndim < 0 || ndim > 8) return fail(CLM_E_ARG, "bad argument");
+  int64_t n = 1;
+  HostTensor t;
+  for (int i = 0; i < ndim; ++i) {
+    if (shape[i] < 0) return fail(CLM_E_ARG, "negative dim");
+    n *= shape[i];
+    t.shape.push_back(shape[i]);
+  }
+  t.data.resize(n);
+  if (dtype == CLM_F32) {
+    std::memcpy(t.data.data(), host_ptr, n * sizeof(float));
+  } else if (dtype == CLM_F16) {
+    const uint16_t* p = (const uint16_t*)host_ptr;
+    for (int64_t i = 0; i < n; ++i) t.data[i] = host_f16_to_f32(p[i]);
+  } else if (dtype == CLM_BF16) {
+    const uint16_t* p = (const uint16_t*)host_ptr;
+    for (int64_t i = 0; i < n; ++i) t.data[i] = host_bf16_to_f32(p[i]);
+  } else {
+    return fail(CLM_E_ARG, "tensor dtype must be f32/f16/bf16");
+  }
+  ctx->host[name] = std::move(t);
+  ctx->finalized = false;
+  return CLM_OK;
+}
+
+int clm_finalize(clm_ctx* ctx) {
+  if (!ctx) return fail(CLM_E_ARG, "null ctx");
+  DeviceGuard g(ctx->dev);
+  (void)hipDeviceSynchronize();
+  ctx->free_all();
+  ctx->finalized = false;
+  int r = build_tower(ctx, ctx->vis, true);
+  if (!r) r = build_tower(ctx, ctx->txt, false);
+  if (!r) r = ctx->dalloc(&ctx->ids_dev, (size_t)ctx->desc.max_batch * ctx->desc.max_pos);
+  if (r) {
+    ctx->free_all();
+    return r;
+  }
+  ctx->finalized = true;
+  return CLM_OK;
+}
+
+int clm_set_lora_enabled(clm_ctx* ctx, int enabled) {
+  if (!ctx) return fail(CLM_E_ARG, "null ctx");
+  ctx->lora_enabled = enabled != 0;
+  return clm_finalize(ctx);
+}
+
+int clm_encode_image(clm_ctx* ctx, const void* pixels, int pix_layout, int n, void* out, int out_dtype,
+                     int normalize, void* stream) {
+  if (!ctx) return fail(CLM_E_ARG, "null ctx");
+  if (!ctx->finalized) return fail(CLM_E_STATE, "clm_finalize has not been called");
+  if (n < 0 || (n > 0 && (!pixels || !out))) return fail(CLM_E_ARG, "bad pixels/out/n");
+  if (pix_layout != CLM_PIX_U8_HWC && pix_layout != CLM_PIX_F32_CHW) return fail(CLM_E_ARG, "bad pix_layout");
+  if (out_dtype != CLM_F32 && out_dtype != CLM_F16) return fail(CLM_E_ARG, "out_dtype must be f32 or f16");
+  if (n == 0) return CLM_OK;
+  DeviceGuard g(ctx->dev);
+  hipStream_t st = (hipStream_t)stream;
+  const clm_model_desc& d = ctx->desc;
+  const size_t pix_bytes = (size_t)d.image_size * d.image_size * d.channels * (pix_layout == CLM_PIX_U8_HWC ? 1 : 4);
+  const size_t out_row = (size_t)d.proj_dim * dtype_size(out_dtype);
+  const bool in_dev = is_device_ptr(pixels), out_dev = is_device_ptr(out);
+  const int mb = d.max_batch;
+  if (!in_dev) {
+    int r = ensure_stage(&ctx->stage_in, &ctx->stage_in_bytes, pix_bytes * mb);
+    if (r) return r;
+  }
+  if (!out_dev) {
+    int r = ensure_stage(&ctx->stage_out, &ctx->stage_out_bytes, out_row * mb);
+    if (r) return r;
+  }
+  for (int i0 = 0; i0 < n; i0 += mb) {
+    const int B = std::min(mb, n - i0);
+    const void* src = (const uint8_t*)pixels + (size_t)i0 * pix_bytes;
+    if (!in_dev) {
+      HIPCHK(hipMemcpyAsync(ctx->stage_in, src, pix_bytes * B, hipMemcpyHostToDevice, st));
+      src = ctx->stage_in;
+    }
+    void* dst = out_dev ? (void*)((uint8_t*)out + (size_t)i0 * out_row) : ctx->stage_out;
+    int r = encode_image_chunk(ctx, src, pix_layout, B, dst, out_dtype, normalize, st);
+    if (r) return r;
+    if (!out_dev) {
+      HIPCHK(hipMemcpyAsync((uint8_t*)out + (size_t)i0 * out_row, ctx->stage_out, out_row * B, hipMemcpyDeviceToHost, st));
+      HIPCHK(hipStreamSynchronize(st));
+    } else if (!in_dev) {
+      HIPCHK(hipStreamSynchronize(st));  // staging buffer reused next chunk
+    }
+  }
+  return CLM_OK;
+}
+
+int clm_encode_text(clm_ctx* ctx, const int32_t* ids, int n, int L, void* out, int out_dtype, int normalize,
+                    void* stream) {
+  if (!ctx) return fail(CLM_E_ARG, "null ctx");
+  if (!ctx->finalized) return fail(CLM_E_STATE, "clm_finalize has not been called");
+  const clm_model_desc& d = ctx->desc;
+  if (n < 0 || (n > 0 && (!ids || !out))) return fail(CLM_E_ARG, "bad ids/out/n");
+  if (L <= 0 || L > d.max_pos)
+    return fail(CLM_E_ARG, "sequence length " + std::to_string(L) + " outside [1, " + std::to_string(d.max_pos) + "]");
+  if (out_dtype != CLM_F32 && out_dtype != CLM_F16) return fail(CLM_E_ARG, "out_dtype must be f32 or f16");
+  if (n == 0) return CLM_OK;
+  DeviceGuard g(ctx->dev);
+  hipStream_t st = (hipStream_t)stream;
+  const size_t out_row = (size_t)d.proj_dim * dtype_size(out_dtype);
+  const bool in_dev = is_device_ptr(ids), out_dev = is_device_ptr(out);
+  const int mb = d.max_batch;
+  if (!out_dev) {
+    int r = ensure_stage(&ctx->stage_out, &ctx->stage_out_bytes, out_row * mb);
+    if (r) return r;
+  }
+  for (int i0 = 0; i0 < n; i0 += mb) {
+    const int B = std::min(mb, n - i0);
+    const int32_t* src = ids + (size_t)i0 * L;
+    if (!in_dev) {
+      for (int64_t q = 0; q < (int64_t)B * L; ++q)
+        if (src[q] < 0 || src[q] >= d.vocab) return fail(CLM_E_ARG, "token id out of range");
+      HIPCHK(hipMemcpyAsync(ctx->ids_dev, src, sizeof(int32_t) * B * L, hipMemcpyHostToDevice, st));
+      src = ctx->ids_dev;
+    }
+    void* dst = out_dev ? (void*)((uint8_t*)out + (size_t)i0 * out_row) : ctx->stage_out;
+    int r = encode_text_chunk(ctx, src, B, L, dst, out_dtype, normalize, st);
+    if (r) return r;
+    if (!out_dev) {
+      HIPCHK(hipMemcpyAsync((uint8_t*)out + (size_t)i0 * out_row, ctx->stage_out, out_row * B, hipMemcpyDeviceToHost, st));
+      HIPCHK(hipStreamSynchronize(st));
+    } else if (!in_dev) {
+      HIPCHK(hipStreamSynchronize(st));
+    }
+  }
+  return CLM_OK;
+}
+
+// ------------------------------------------------------------------ index ---
+int clm_index_create(int hip_device, int64_t capacity, int dim, clm_index** out) {
+  if (!out || capacity < 0 || dim <= 0 || dim % 64) return fail(CLM_E_ARG, "bad capacity/dim (dim must be a multiple of 64)");
+  DeviceGuard g(hip_device);
+  clm_index* x = new clm_index();
+  x->dev = hip_device;
+  x->cap = std::max<int64_t>(capacity, 1);
+  x->dim = dim;
+  if (hipMalloc(&x->rows, (size_t)x->cap * dim * sizeof(u16)) != hipSuccess ||
+      hipMalloc(&x->inv, (size_t)x->cap * sizeof(float)) != hipSuccess) {
+    (void)hipGetLastError();
+    if (x->rows) (void)hipFree(x->rows);
+    delete x;
+    return fail(CLM_E_OOM, "index allocation failed");
+  }
+  *out = x;
+  return CLM_OK;
+}
+
+int clm_index_destroy(clm_index* x) {
+  if (!x) return CLM_OK;
+  DeviceGuard g(x->dev);
+  (void)hipDeviceSynchronize();
+  if (x->rows) (void)hipFree(x->rows);
+  if (x->inv) (void)hipFree(x->inv);
+  if (x->ws) (void)hipFree(x->ws);
+  delete x;
+  return CLM_OK;
+}
+
+static int index_grow(clm_index* x, int64_t need_rows) {
+  if (need_rows <= x->cap) return CLM_OK;
+  int64_t nc = std::max<int64_t>(need_rows, x->cap * 2);
+  u16* nr = nullptr;
+  float* ni = nullptr;
+  if (hipMalloc(&nr, (size_t)nc * x->dim * sizeof(u16)) != hipSuccess ||
+      hipMalloc(&ni, (size_t)nc * sizeof(float)) != hipSuccess) {
+    (void)hipGetLastError();
+    if (nr) (void)hipFree(nr);
+    return fail(CLM_E_OOM, "index grow failed");
+  }
+  HIPCHK(hipMemcpy(nr, x->rows, (size_t)x->n * x->dim * sizeof(u16), hipMemcpyDeviceToDevice));
+  HIPCHK(hipMemcpy(ni, x->inv, (size_t)x->n * sizeof(float), hipMemcpyDeviceToDevice));
+  (void)hipFree(x->rows);
+  (void)hipFree(x->inv);
+  x->rows = nr;
+  x->inv = ni;
+  x->cap = nc;
+  return CLM_OK;
+}
+
+int clm_index_append(clm_index* x, const void* rows, int dtype, int64_t n, void* stream) {
+  if (!x || n < 0 || (n > 0 && !rows)) return fail(CLM_E_ARG, "bad argument");
+  if (dtype != CLM_F32 && dtype != CLM_F16) return fail(CLM_E_ARG, "rows must be f32 or f16");
+  if (n == 0) return CLM_OK;
+  DeviceGuard g(x->dev);
+  hipStream_t st = (hipStream_t)stream;
+  HIPCHK(hipStreamSynchronize(st));
+  int r = index_grow(x, x->n + n);
+  if (r) return r;
+  const size_t bytes = (size_t)n * x->dim * dtype_size(dtype);
+  const void* src = rows;
+  void* tmp = nullptr;
+  if (!is_device_ptr(rows)) {
+    if (hipMalloc(&tmp, bytes) != hipSuccess) { (void)hipGetLastError(); return fail(CLM_E_OOM, "staging failed"); }
+    HIPCHK(hipMemcpyAsync(tmp, rows, bytes, hipMemcpyHostToDevice, st));
+    src = tmp;
+  }
+  // inverse norm of the fp16-ROUNDED row: the reference re-normalises the fp32
+  // upcast of the stored rows at load (search.py:36,68)
+  hipError_t e = rows_to_f16(src, dtype == CLM_F32 ? 0 : 1, n, (int)x->dim, x->rows + (size_t)x->n * x->dim,
+                             x->inv + x->n, st, 0);
+  if (tmp) {
+    (void)hipStreamSynchronize(st);
+    (void)hipFree(tmp);
+  }
+  if (e != hipSuccess) return fail(CLM_E_HIP, std::string("rows_to_f16: ") + hipGetErrorString(e));
+  x->n += n;
+  return CLM_OK;
+}
+
+int64_t clm_index_size(const clm_index* x) { return x ? x->n : -1; }
+
+int clm_index_reset(clm_index* x) {
+  if (!x) return fail(CLM_E_ARG, "null index");
+  x->n = 0;
+  return CLM_OK;
+}
+
+int clm_index_set_offset(clm_index* x, int64_t off) {
+  if (!x || off < 0) return fail(CLM_E_ARG, "bad argument");
+  x->offset = off;
+  return CLM_OK;
+}
+
+int clm_index_read(clm_index* x, int64_t start, int64_t n, float* dst, void* stream) {
+  if (!x || start < 0 || n < 0 || start + n > x->n || (n > 0 && !dst)) return fail(CLM_E_ARG, "bad range");
+  if (n == 0) return CLM_OK;
+  DeviceGuard g(x->dev);
+  hipStream_t st = (hipStream_t)stream;
+  std::vector<u16> h((size_t)n * x->dim);
+  HIPCHK(hipMemcpyAsync(h.data(), x->rows + (size_t)start * x->dim, h.size() * 2, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
+  std::vector<float> f(h.size());
+  for (size_t i = 0; i < h.size(); ++i) f[i] = host_f16_to_f32(h[i]);
+  if (is_device_ptr(dst)) {
+    HIPCHK(hipMemcpy(dst, f.data(), f.size() * 4, hipMemcpyHostToDevice));
+  } else {
+    std::memcpy(dst, f.data(), f.size() * 4);
+  }
+  return CLM_OK;
+}
+
+static int ws_ensure(clm_index* x, size_t bytes) {
+  if (x->ws_bytes >= bytes) return CLM_OK;
+  if (x->ws) (void)hipFree(x->ws);
+  x->ws = nullptr;
+  x->ws_bytes = 0;
+  if (hipMalloc(&x->ws, bytes) != hipSuccess) {
+    (void)hipGetLastError();
+    return fail(CLM_E_OOM, "search workspace allocation failed");
+  }
+  x->ws_bytes = bytes;
+  return CLM_OK;
+}
+
+// queries -> fp16 rows + fp32 inverse norms of the source values (for a query the scale only
+// changes the score value, never the order)
+int clm_index_search(clm_index* x, const void* q, int q_dtype, int64_t nq, int k, float* out_scores,
+                     int64_t* out_idx, void* stream) {
+  if (!x || nq < 0 || (nq > 0 && (!q || !out_scores || !out_idx))) return fail(CLM_E_ARG, "bad argument");
+  if (q_dtype != CLM_F32 && q_dtype != CLM_F16) return fail(CLM_E_ARG, "queries must be f32 or f16");
+  if (k < 1 || k > 1024) return fail(CLM_E_ARG, "k must be in [1, 1024]");
+  if (nq == 0) return CLM_OK;
+  DeviceGuard g(x->dev);
+  hipStream_t st = (hipStream_t)stream;
+  const int dim = (int)x->dim;
+  const int64_t N = x->n;
+  const bool q_dev = is_device_ptr(q);
+  const bool o_dev = is_device_ptr(out_scores) && is_device_ptr(out_idx);
+
+  // chunking: nchunks * k <= 8192 (merge sort size), score buffer <= budget
+  const size_t budget = (size_t)512 << 20;
+  const int64_t max_chunks = std::max<int64_t>(1, 8192 / k);
+  int64_t ch = std::max<int64_t>(1, N);
+  if (N > 0) {
+    ch = std::max<int64_t>((N + max_chunks - 1) / max_chunks, std::min<int64_t>(N, 1 << 17));
+    ch = round_up(ch, 128);
+  }
+  const int64_t nchunks = N > 0 ? (N + ch - 1) / ch : 0;
+  int64_t nqb = std::max<int64_t>(1, std::min<int64_t>(nq, (int64_t)(budget / ((size_t)ch * 4))));
+  nqb = std::min<int64_t>(nqb, 4096);
+
+  // workspace layout: q16 [nq, dim] | qinv [nq] | scores [nqb, ch] | cand_s/cand_i [nqb, nchunks*k] | out staging
+  const size_t q_src_bytes = (size_t)nq * dim * (q_dtype == CLM_F32 ? 4 : 2);
+  size_t off = 0;
+  auto take = [&](size_t bytes) { size_t o = off; off = round_up(off + bytes, 256); return o; };
+  const size_t o_qsrc = q_dev ? 0 : take(q_src_bytes);
+  const size_t o_q16 = take((size_t)nq * dim * 2);
+  const size_t o_qinv = take((size_t)nq * 4);
+  const size_t o_sc = take((size_t)nqb * std::max<int64_t>(ch, 1) * 4);
+  const size_t o_cs = take((size_t)nqb * std::max<int64_t>(nchunks, 1) * k * 4);
+  const size_t o_ci = take((size_t)nqb * std::max<int64_t>(nchunks, 1) * k * 8);
+  const size_t o_os = o_dev ? 0 : take((size_t)nq * k * 4);
+  const size_t o_oi = o_dev ? 0 : take((size_t)nq * k * 8);
+  int r = ws_ensure(x, off);
+  if (r) return r;
+  uint8_t* ws = (uint8_t*)x->ws;
+  const void* qsrc = q;
+  if (!q_dev) {
+    HIPCHK(hipMemcpyAsync(ws + o_qsrc, q, q_src_bytes, hipMemcpyHostToDevice, st));
+    qsrc = ws + o_qsrc;
+  }
+  u16* q16 = (u16*)(ws + o_q16);
+  float* qinv = (float*)(ws + o_qinv);
+  // inverse norms of the SOURCE rows (reference normalises the fp32 query, search.py:93)
+  KCHK(rows_to_f16(qsrc, q_dtype == CLM_F32 ? 0 : 1, nq, dim, q16, qinv, st, 1));
+  float* osc = o_dev ? out_scores : (float*)(ws + o_os);
+  int64_t* oix = o_dev ? out_idx : (int64_t*)(ws + o_oi);
+  float* sc = (float*)(ws + o_sc);
+  float* cs = (float*)(ws + o_cs);
+  int64_t* ci = (int64_t*)(ws + o_ci);
+  for (int64_t q0 = 0; q0 < nq; q0 += nqb) {
+    const int64_t nb = std::min(nqb, nq - q0);
+    if (N == 0) {
+      KCHK(topk_rows(sc, 1, nb, 0, k, 0, osc + q0 * k, oix + q0 * k, k, st));
+      continue;
+    }
+    for (int64_t c = 0; c < nchunks; ++c) {
+      const int64_t r0 = c * ch, rn = std::min(ch, N - r0);
+      GemmArgs ga{};
+      ga.A = q16 + q0 * dim; ga.lda = dim; ga.W = x->rows + r0 * dim; ga.ldw = dim;
+      ga.M = (int)nb; ga.N = (int)rn; ga.K = dim; ga.out = sc; ga.ldo = ch;
+      ga.rscale = qinv + q0; ga.cscale = x->inv + r0;
+      KCHK(gemm(false, EPI_SCORE, ga, st));
+      if (nchunks == 1) {
+        KCHK(topk_rows(sc, ch, nb, rn, k, x->offset + r0, osc + q0 * k, oix + q0 * k, k, st));
+      } else {
+        KCHK(topk_rows(sc, ch, nb, rn, k, x->offset + r0, cs + c * k, ci + c * k, nchunks * k, st));
+      }
+    }
+    if (nchunks > 1) KCHK(topk_merge(cs, ci, nb, (int)nchunks, k, k, osc + q0 * k, oix + q0 * k, st));
+  }
+  if (!o_dev) {
+    HIPCHK(hipMemcpyAsync(out_scores, osc, (size_t)nq * k * 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(out_idx, oix, (size_t)nq * k * 8, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+  } else if (!q_dev) {
+    HIPCHK(hipStreamSynchronize(st));
+  }
+  return CLM_OK;
+}
+
+int clm_cosine_scores(int hip_device, const float* q, int64_t nq, const float* c, int64_t n, int dim, float* out,
+                      void* stream) {
+  if (nq < 0 || n < 0 || dim <= 0 || dim % 64 || (nq * n > 0 && (!q || !c || !out)))
+    return fail(CLM_E_ARG, "bad argument (dim must be a multiple of 64)");
+  if (nq == 0 || n == 0) return CLM_OK;
+  DeviceGuard g(hip_device);
+  hipStream_t st = (hipStream_t)stream;
+  const bool qd = is_device_ptr(q), cd = is_device_ptr(c), od = is_device_ptr(out);
+  size_t bytes = (size_t)(nq + n) * dim * 2 + (size_t)(nq + n) * 4 + (qd ? 0 : (size_t)nq * dim * 4) +
+                 (cd ? 0 : (size_t)n * dim * 4) + (od ? 0 : (size_t)nq * n * 4) + 1024;
+  uint8_t* w = nullptr;
+  if (hipMalloc(&w, bytes) != hipSuccess) { (void)hipGetLastError(); return fail(CLM_E_OOM, "workspace"); }
+  size_t off = 0;
+  auto take = [&](size_t b) { size_t o = off; off = round_up(off + b, 256); return w + o; };
+  u16* q16 = (u16*)take((size_t)nq * dim * 2);
+  u16* c16 = (u16*)take((size_t)n * dim * 2);
+  float* qi = (float*)take((size_t)nq * 4);
+  float* cinv = (float*)take((size_t)n * 4);
+  const float* qs = q;
+  const float* cs = c;
+  float* os = out;
+  int rc = CLM_OK;
+  hipError_t e = hipSuccess;
+  if (!qd) { float* t = (float*)take((size_t)nq * dim * 4); e = hipMemcpyAsync(t, q, (size_t)nq * dim * 4, hipMemcpyHostToDevice, st); qs = t; }
+  if (e == hipSuccess && !cd) { float* t = (float*)take((size_t)n * dim * 4); e = hipMemcpyAsync(t, c, (size_t)n * dim * 4, hipMemcpyHostToDevice, st); cs = t; }
+  if (!od) os = (float*)take((size_t)nq * n * 4);
+  if (e == hipSuccess) e = rows_to_f16(qs, 0, nq, dim, q16, qi, st, 1);
+  if (e == hipSuccess) e = rows_to_f16(cs, 0, n, dim, c16, cinv, st, 1);
+  if (e == hipSuccess) {
+    GemmArgs ga{};
+    ga.A = q16; ga.lda = dim; ga.W = c16; ga.ldw = dim; ga.M = (int)nq; ga.N = (int)n; ga.K = dim;
+    ga.out = os; ga.ldo = n; ga.rscale = qi; ga.cscale = cinv;
+    e = gemm(false, EPI_SCORE, ga, st);
+  }
+  if (e == hipSuccess && !od) e = hipMemcpyAsync(out, os, (size_t)nq * n * 4, hipMemcpyDeviceToHost, st);
+  if (e == hipSuccess) e = hipStreamSynchronize(st);
+  if (e != hipSuccess) rc = fail(CLM_E_HIP, std::string("cosine_scores: ") + hipGetErrorString(e));
+  (void)hipFree(w);
+  return rc;
+}
+
+int clm_topk_merge(int hip_device, const float* scores, const int64_t* idx, int64_t nq, int parts, int k_in, int k,
+                   float* out_scores, int64_t* out_idx, void* stream) {
+  if (nq < 0 || parts <= 0 || k_in <= 0 || k <= 0 || k > 1024 || (int64_t)parts * k_in > 8192)
+    return fail(CLM_E_ARG, "bad merge shape (parts*k_in <= 8192, k <= 1024)");
+  if (nq == 0) return CLM_OK;
+  DeviceGuard g(hip_device);
+  hipStream_t st = (hipStream_t)stream;
+  const bool in_d = is_device_ptr(scores) && is_device_ptr(idx);
+  const bool out_d = is_device_ptr(out_scores) && is_device_ptr(out_idx);
+  const size_t n_in = (size_t)nq * parts * k_in;
+  uint8_t* w = nullptr;
+  const size_t bytes = (in_d ? 0 : n_in * 12) + (out_d ? 0 : (size_t)nq * k * 12) + 512;
+  if (bytes > 512 && hipMalloc(&w, bytes) != hipSuccess) { (void)hipGetLastError(); return fail(CLM_E_OOM, "workspace"); }
+  size_t off = 0;
+  auto take = [&](size_t b) { size_t o = off; off = round_up(off + b, 256); return w + o; };
+  const float* s_in = scores;
+  const int64_t* i_in = idx;
+  float* s_out = out_scores;
+  int64_t* i_out = out_idx;
+  hipError_t e = hipSuccess;
+  if (!in_d) {
+    float* a = (float*)take(n_in * 4);
+    int64_t* b = (int64_t*)take(n_in * 8);
+    e = hipMemcpyAsync(a, scores, n_in * 4, hipMemcpyHostToDevice, st);
+    if (e == hipSuccess) e = hipMemcpyAsync(b, idx, n_in * 8, hipMemcpyHostToDevice, st);
+    s_in = a; i_in = b;
+  }
+  if (!out_d) { s_out = (float*)take((size_t)nq * k * 4); i_out = (int64_t*)take((size_t)nq * k * 8); }
+  if (e == hipSuccess) e = topk_merge(s_in, i_in, nq, parts, k_in, k, s_out, i_out, st);
+  if (e == hipSuccess && !out_d) {
+    e = hipMemcpyAsync(out_scores, s_out, (size_t)nq * k * 4, hipMemcpyDeviceToHost, st);
+    if (e == hipSuccess) e = hipMemcpyAsync(out_idx, i_out, (size_t)nq * k * 8, hipMemcpyDeviceToHost, st);
+  }
+  if (e == hipSuccess && (!in_d || !out_d)) e = hipStreamSynchronize(st);
+  if (w) (void)hipFree(w);
+  if (e != hipSuccess) return fail(CLM_E_HIP, std::string("topk_merge: ") + hipGetErrorString(e));
+  return CLM_OK;
+}
+
+int clm_l2_normalize(int hip_device, float* rows, int64_t n, int dim, void* stream) {
+  if (n < 0 || dim <= 0 || (n > 0 && !rows)) return fail(CLM_E_ARG, "bad argument");
+  if (n == 0) return CLM_OK;
+  DeviceGuard g(hip_device);
+  hipStream_t st = (hipStream_t)stream;
+  if (is_device_ptr(rows)) {
+    KCHK(l2_normalize_rows(rows, n, dim, st));
+    return CLM_OK;
+  }
+  float* t = nullptr;
+  if (hipMalloc(&t, (size_t)n * dim * 4) != hipSuccess) { (void)hipGetLastError(); return fail(CLM_E_OOM, "workspace"); }
+  hipError_t e = hipMemcpyAsync(t, rows, (size_t)n * dim * 4, hipMemcpyHostToDevice, st);
+  if (e == hipSuccess) e = l2_normalize_rows(t, n, dim, st);
+  if (e == hipSuccess) e = hipMemcpyAsync(rows, t, (size_t)n * dim * 4, hipMemcpyDeviceToHost, st);
+  if (e == hipSuccess) e = hipStreamSynchronize(st);
+  (void)hipFree(t);
+  if (e != hipSuccess) return fail(CLM_E_HIP, std::string("l2_normalize: ") + hipGetErrorString(e));
+  return CLM_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,79 @@
+// Common device/host helpers for libclm (gfx950 / CDNA4 only).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+typedef uint16_t u16;
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+namespace clm {
+
+constexpr int WAVE = 64;
+
+// ---- scalar conversions (RNE; NaN preserved by the hardware cvt) ----------
+__device__ __forceinline__ float bf16_to_f32(u16 v) { return __uint_as_float(((uint32_t)v) << 16); }
+__device__ __forceinline__ float f16_to_f32(u16 v) { return (float)__builtin_bit_cast(_Float16, v); }
+__device__ __forceinline__ u16 f32_to_bf16(float f) { return __builtin_bit_cast(u16, (__bf16)f); }
+__device__ __forceinline__ u16 f32_to_f16(float f) { return __builtin_bit_cast(u16, (_Float16)f); }
+
+template <bool BF> __device__ __forceinline__ float to_f32(u16 v) { return BF ? bf16_to_f32(v) : f16_to_f32(v); }
+template <bool BF> __device__ __forceinline__ u16 from_f32(float f) { return BF ? f32_to_bf16(f) : f32_to_f16(f); }
+
+// pack two floats into one dword of two 16-bit values (lo first)
+template <bool BF> __device__ __forceinline__ uint32_t pack2(float a, float b) {
+  return (uint32_t)from_f32<BF>(a) | ((uint32_t)from_f32<BF>(b) << 16);
+}
+
+// one 16x16x32 MFMA on 8-element fragments held as raw 16-byte vectors
+template <bool BF>
+__device__ __forceinline__ f32x4 mfma16(const u32x4& a, const u32x4& b, f32x4 c) {
+  if constexpr (BF)
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a),
+                                                   __builtin_bit_cast(bf16x8, b), c, 0, 0, 0);
+  else
+    return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, a),
+                                                  __builtin_bit_cast(f16x8, b), c, 0, 0, 0);
+}
+
+// ---- wave reductions (64 lanes) ---------------------------------------------
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+// reductions inside aligned groups of 16 lanes (MFMA C-layout rows)
+__device__ __forceinline__ float group16_sum(float v) {
+#pragma unroll
+  for (int o = 8; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ float group16_max(float v) {
+#pragma unroll
+  for (int o = 8; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+__device__ __forceinline__ float quick_gelu(float x) {
+  // TF/activations.py:123  x * sigmoid(1.702 x)
+  return x / (1.0f + __expf(-1.702f * x));
+}
+
+// XOR swizzle of 16-byte chunks inside 128-byte LDS rows: conflict-free
+// ds_read_b128 for MFMA fragment reads of 16 consecutive rows.
+__device__ __forceinline__ int swz(int row, int chunk) { return chunk ^ ((row >> 1) & 7); }
+
+// bijective XCD-aware remap of a linear workgroup id (cdna_hip_programming §5 T1)
+__device__ __forceinline__ int xcd_remap(int bid, int nwg) {
+  const int q = nwg / 8, r = nwg % 8, x = bid % 8;
+  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + bid / 8;
+}
+
+}  // namespace clm

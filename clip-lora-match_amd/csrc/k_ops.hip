@@ -1,0 +1,361 @@
+// Row-wise kernels of the encode path (gfx950): LayerNorm (+ fused text
+// embedding gather, + fused LoRA down-projection), patchify with the
+// CLIPProcessor rescale/normalise fused, CLS assembly, and the pooled-row
+// LN -> projection -> L2-normalise tail.
+//
+// Reference arithmetic (TF = transformers/):
+//   LayerNorm eps 1e-5             TF/models/clip/modeling_clip.py:358,360,605,607,504
+//   text embeddings gather+add     modeling_clip.py:232-256
+//   vision embeddings cls/pos      modeling_clip.py:202-218
+//   rescale/normalize              TF/image_transforms.py rescale (f64 mul -> f32), normalize
+//   pooled CLS / first-EOS row     modeling_clip.py:561-582, 650-651
+//   projection + L2 norm           modeling_clip.py:712-713,750-751; models/clip_model.py:116,148
+//   PEFT LoRA down-projection x.A^T (lora_A), models/clip_model.py:78
+#include "kernels.hpp"
+
+namespace clm {
+
+namespace {
+
+// ------------------------------------------------------------------ LN ------
+// One wave per row; lane owns NP float2 pairs at e = (i*64 + lane)*2.
+template <bool BF, int NP>
+__global__ __launch_bounds__(256) void ln_kernel(LnArgs a) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= a.M) return;
+  const int d = NP * 128;
+  float x[NP][2];
+  if (a.mode == 0) {
+    const float* src = a.src + (int64_t)row * a.lds;
+#pragma unroll
+    for (int i = 0; i < NP; ++i) {
+      const float2 v = *(const float2*)(src + (i * 64 + lane) * 2);
+      x[i][0] = v.x; x[i][1] = v.y;
+    }
+  } else {
+    const int tokid = a.ids[row];
+    const float* tk = a.tok + (int64_t)tokid * d;
+    const float* ps = a.pos + (int64_t)(row % a.L) * d;
+#pragma unroll
+    for (int i = 0; i < NP; ++i) {
+      const int e = (i * 64 + lane) * 2;
+      const float2 t = *(const float2*)(tk + e);
+      const float2 p = *(const float2*)(ps + e);
+      x[i][0] = t.x + p.x; x[i][1] = t.y + p.y;
+    }
+  }
+  auto ln = [&](const float* g, const float* b) {
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < NP; ++i) s += x[i][0] + x[i][1];
+    const float mean = wave_sum(s) / d;
+    float v = 0.f;
+#pragma unroll
+    for (int i = 0; i < NP; ++i) {
+      const float d0 = x[i][0] - mean, d1 = x[i][1] - mean;
+      v += d0 * d0 + d1 * d1;
+    }
+    const float rstd = 1.0f / sqrtf(wave_sum(v) / d + a.eps);
+#pragma unroll
+    for (int i = 0; i < NP; ++i) {
+      const int e = (i * 64 + lane) * 2;
+      const float2 gg = *(const float2*)(g + e);
+      const float2 bb = *(const float2*)(b + e);
+      x[i][0] = (x[i][0] - mean) * rstd * gg.x + bb.x;
+      x[i][1] = (x[i][1] - mean) * rstd * gg.y + bb.y;
+    }
+  };
+  auto store_h = [&]() {
+    float* h = a.hf + (int64_t)row * a.ldh;
+#pragma unroll
+    for (int i = 0; i < NP; ++i) *(float2*)(h + (i * 64 + lane) * 2) = make_float2(x[i][0], x[i][1]);
+  };
+  if (a.g2) {
+    ln(a.g1, a.b1);
+    store_h();
+    ln(a.g2, a.b2);
+  } else {
+    if (a.mode == 1) store_h();
+    ln(a.g1, a.b1);
+  }
+  u16* y = a.y + (int64_t)row * a.ldy;
+#pragma unroll
+  for (int i = 0; i < NP; ++i) *(uint32_t*)(y + (i * 64 + lane) * 2) = pack2<BF>(x[i][0], x[i][1]);
+
+  if (a.loraA) {  // y[:, d + j] = sum_e x_e * A[j, e]
+    float mine = 0.f;
+    for (int j = 0; j < a.r_ext; ++j) {
+      const float* A = a.loraA + (int64_t)j * d;
+      float s = 0.f;
+#pragma unroll
+      for (int i = 0; i < NP; ++i) {
+        const float2 w = *(const float2*)(A + (i * 64 + lane) * 2);
+        s += x[i][0] * w.x + x[i][1] * w.y;
+      }
+      s = wave_sum(s);
+      if (lane == j) mine = s;
+    }
+    if (lane < a.r_pad) y[d + lane] = from_f32<BF>(lane < a.r_ext ? mine : 0.f);
+  }
+}
+
+template <bool BF>
+hipError_t ln_dispatch(const LnArgs& a, hipStream_t s) {
+  dim3 grid((a.M + 3) / 4), block(256);
+  switch (a.d) {
+    case 128: ln_kernel<BF, 1><<<grid, block, 0, s>>>(a); break;
+    case 256: ln_kernel<BF, 2><<<grid, block, 0, s>>>(a); break;
+    case 512: ln_kernel<BF, 4><<<grid, block, 0, s>>>(a); break;
+    case 768: ln_kernel<BF, 6><<<grid, block, 0, s>>>(a); break;
+    case 1024: ln_kernel<BF, 8><<<grid, block, 0, s>>>(a); break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+// -------------------------------------------------------------- lora_down --
+template <bool BF>
+__global__ __launch_bounds__(256) void lora_down_kernel(u16* X, int64_t ldx, int M, int K,
+                                                        const float* A, int r_ext, int r_pad) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= M) return;
+  u16* x = X + (int64_t)row * ldx;
+  float mine = 0.f;
+  for (int j = 0; j < r_ext; ++j) {
+    const float* a = A + (int64_t)j * K;
+    float s = 0.f;
+    for (int e = lane * 2; e < K; e += 128) {
+      const uint32_t pr = *(const uint32_t*)(x + e);
+      const float2 w = *(const float2*)(a + e);
+      s += to_f32<BF>((u16)(pr & 0xffff)) * w.x + to_f32<BF>((u16)(pr >> 16)) * w.y;
+    }
+    s = wave_sum(s);
+    if (lane == j) mine = s;
+  }
+  if (lane < r_pad) x[K + lane] = from_f32<BF>(lane < r_ext ? mine : 0.f);
+}
+
+// -------------------------------------------------------------- patchify ---
+// One thread per 8 consecutive K entries of one patch row.
+template <bool BF>
+__global__ __launch_bounds__(256) void patchify_kernel(const void* pix, int layout, int B, int S, int p,
+                                                       int C, const float* lut, u16* P, int Kp) {
+  const int G = S / p;
+  const int64_t rows = (int64_t)B * G * G;
+  const int chunks = Kp / 8;
+  const int64_t total = rows * chunks;
+  const int pp = p * p, kreal = C * pp;
+  for (int64_t w = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; w < total;
+       w += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = w / chunks;
+    const int kc = (int)(w - r * chunks);
+    const int b = (int)(r / (G * G));
+    const int pi = (int)(r - (int64_t)b * G * G);
+    const int py = pi / G, px = pi - py * G;
+    float v[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int k = kc * 8 + e;
+      float val = 0.f;
+      if (k < kreal) {
+        const int c = k / pp, rem = k - c * pp;
+        const int ky = rem / p, kx = rem - ky * p;
+        const int yy = py * p + ky, xx = px * p + kx;
+        if (layout == 0) {
+          const uint8_t u = ((const uint8_t*)pix)[(((int64_t)b * S + yy) * S + xx) * C + c];
+          val = lut[c * 256 + u];
+        } else {
+          val = ((const float*)pix)[(((int64_t)b * C + c) * S + yy) * S + xx];
+        }
+      }
+      v[e] = val;
+    }
+    uint4 o;
+    o.x = pack2<BF>(v[0], v[1]); o.y = pack2<BF>(v[2], v[3]);
+    o.z = pack2<BF>(v[4], v[5]); o.w = pack2<BF>(v[6], v[7]);
+    *(uint4*)(P + r * Kp + kc * 8) = o;
+  }
+}
+
+__global__ void write_cls_kernel(float* h, int64_t ldh, int B, int T, int d, const float* cls,
+                                 const float* pos) {
+  const int b = blockIdx.x;
+  for (int e = threadIdx.x; e < d; e += blockDim.x) h[(int64_t)b * T * ldh + e] = cls[e] + pos[e];
+}
+
+// ------------------------------------------------------- pool + projection --
+__device__ __forceinline__ float block_sum256(float v, float* red) {
+  v = wave_sum(v);
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  __syncthreads();
+  if (lane == 0) red[wid] = v;
+  __syncthreads();
+  return red[0] + red[1] + red[2] + red[3];
+}
+
+__global__ __launch_bounds__(256) void pool_project_kernel(const float* h, int64_t ldh, int T, int d,
+                                                           const int32_t* ids, int eos, const float* g,
+                                                           const float* bt, float eps, const float* projT,
+                                                           int D, void* out, int out_dtype, int normalize) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  float* y = sm;            // d
+  float* red = sm + d;      // 8
+  __shared__ int pos_s;
+  __shared__ int maxv_s;
+  const int b = blockIdx.x, tid = threadIdx.x;
+  int prow = 0;
+  if (ids) {
+    const int32_t* id = ids + (int64_t)b * T;
+    if (tid == 0) { pos_s = INT_MAX; maxv_s = INT_MIN; }
+    __syncthreads();
+    if (eos == 2) {  // legacy rule: argmax(ids), first occurrence
+      for (int t = tid; t < T; t += 256) atomicMax(&maxv_s, id[t]);
+      __syncthreads();
+      for (int t = tid; t < T; t += 256) if (id[t] == maxv_s) atomicMin(&pos_s, t);
+    } else {         // first index of eos; (ids==eos).argmax() is 0 when absent
+      for (int t = tid; t < T; t += 256) if (id[t] == eos) atomicMin(&pos_s, t);
+    }
+    __syncthreads();
+    prow = pos_s == INT_MAX ? 0 : pos_s;
+  }
+  const float* x = h + ((int64_t)b * T + prow) * ldh;
+  float s = 0.f;
+  for (int e = tid; e < d; e += 256) { const float v = x[e]; y[e] = v; s += v; }
+  const float mean = block_sum256(s, red) / d;
+  float v = 0.f;
+  for (int e = tid; e < d; e += 256) { const float t = y[e] - mean; v += t * t; }
+  const float rstd = 1.0f / sqrtf(block_sum256(v, red) / d + eps);
+  for (int e = tid; e < d; e += 256) y[e] = (y[e] - mean) * rstd * g[e] + bt[e];
+  __syncthreads();
+  float o[4] = {0.f, 0.f, 0.f, 0.f};
+  for (int i = 0; i < d; ++i) {
+    const float yi = y[i];
+    const float* pr = projT + (int64_t)i * D;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int j = tid + q * 256;
+      if (j < D) o[q] += yi * pr[j];
+    }
+  }
+  float ss = 0.f;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) if (tid + q * 256 < D) ss += o[q] * o[q];
+  const float nrm = normalize ? sqrtf(block_sum256(ss, red)) : 1.0f;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int j = tid + q * 256;
+    if (j >= D) continue;
+    const float r = normalize ? o[q] / nrm : o[q];
+    if (out_dtype == 0) ((float*)out)[(int64_t)b * D + j] = r;
+    else ((u16*)out)[(int64_t)b * D + j] = f32_to_f16(r);
+  }
+}
+
+// ------------------------------------------------------------ index rows ---
+__global__ __launch_bounds__(256) void rows_to_f16_kernel(const void* src, int src_dtype, int64_t n, int dim,
+                                                          u16* dst, float* inv_norm, int norm_src) {
+  const int lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= n) return;
+  float s = 0.f;
+  for (int e = lane; e < dim; e += 64) {
+    float v;
+    if (src_dtype == 0) v = ((const float*)src)[row * dim + e];
+    else v = f16_to_f32(((const u16*)src)[row * dim + e]);
+    const u16 hv = f32_to_f16(v);
+    dst[row * dim + e] = hv;
+    const float r = norm_src ? v : f16_to_f32(hv);
+    s += r * r;
+  }
+  s = wave_sum(s);
+  if (lane == 0) inv_norm[row] = 1.0f / sqrtf(s);
+}
+
+__global__ __launch_bounds__(256) void l2n_kernel(float* rows, int64_t n, int dim) {
+  const int lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= n) return;
+  float* r = rows + row * dim;
+  float s = 0.f;
+  for (int e = lane; e < dim; e += 64) s += r[e] * r[e];
+  const float nrm = sqrtf(wave_sum(s));
+  for (int e = lane; e < dim; e += 64) r[e] = r[e] / nrm;
+}
+
+__global__ __launch_bounds__(256) void f32_to_f16_kernel(const float* src, int64_t total, u16* dst) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x)
+    dst[i] = f32_to_f16(src[i]);
+}
+
+}  // namespace
+
+hipError_t layernorm(bool bf16, const LnArgs& a, hipStream_t s) {
+  if (a.M <= 0) return hipSuccess;
+  if (a.r_ext > 64 || a.r_pad > 64) return hipErrorInvalidValue;
+  return bf16 ? ln_dispatch<true>(a, s) : ln_dispatch<false>(a, s);
+}
+
+hipError_t lora_down(bool bf16, u16* X, int64_t ldx, int M, int K, const float* A, int r_ext, int r_pad,
+                     hipStream_t s) {
+  if (M <= 0) return hipSuccess;
+  if (r_ext > 64 || r_pad > 64 || (K % 2)) return hipErrorInvalidValue;
+  dim3 grid((M + 3) / 4), block(256);
+  if (bf16) lora_down_kernel<true><<<grid, block, 0, s>>>(X, ldx, M, K, A, r_ext, r_pad);
+  else lora_down_kernel<false><<<grid, block, 0, s>>>(X, ldx, M, K, A, r_ext, r_pad);
+  return hipGetLastError();
+}
+
+hipError_t patchify(bool bf16, const void* pix, int layout, int B, int S, int p, int C, const float* lut,
+                    u16* P, int Kp, hipStream_t s) {
+  if (B <= 0) return hipSuccess;
+  if (Kp % 8) return hipErrorInvalidValue;
+  const int64_t total = (int64_t)B * (S / p) * (S / p) * (Kp / 8);
+  const int blocks = (int)std::min<int64_t>((total + 255) / 256, 256 * 16);
+  if (bf16) patchify_kernel<true><<<blocks, 256, 0, s>>>(pix, layout, B, S, p, C, lut, P, Kp);
+  else patchify_kernel<false><<<blocks, 256, 0, s>>>(pix, layout, B, S, p, C, lut, P, Kp);
+  return hipGetLastError();
+}
+
+hipError_t write_cls(float* h, int64_t ldh, int B, int T, int d, const float* cls, const float* pos,
+                     hipStream_t s) {
+  if (B <= 0) return hipSuccess;
+  write_cls_kernel<<<B, 256, 0, s>>>(h, ldh, B, T, d, cls, pos);
+  return hipGetLastError();
+}
+
+hipError_t pool_project(const float* h, int64_t ldh, int B, int T, int d, const int32_t* ids, int eos,
+                        const float* g, const float* bta, float eps, const float* projT, int D, void* out,
+                        int out_dtype, int normalize, hipStream_t s) {
+  if (B <= 0) return hipSuccess;
+  if (D > 1024) return hipErrorInvalidValue;
+  const size_t sm = (size_t)(d + 8) * sizeof(float);
+  pool_project_kernel<<<B, 256, sm, s>>>(h, ldh, T, d, ids, eos, g, bta, eps, projT, D, out, out_dtype,
+                                         normalize);
+  return hipGetLastError();
+}
+
+hipError_t rows_to_f16(const void* src, int src_dtype, int64_t n, int dim, u16* dst, float* inv_norm,
+                       hipStream_t s, int norm_src) {
+  if (n <= 0) return hipSuccess;
+  rows_to_f16_kernel<<<(unsigned)((n + 3) / 4), 256, 0, s>>>(src, src_dtype, n, dim, dst, inv_norm, norm_src);
+  return hipGetLastError();
+}
+
+hipError_t l2_normalize_rows(float* rows, int64_t n, int dim, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  l2n_kernel<<<(unsigned)((n + 3) / 4), 256, 0, s>>>(rows, n, dim);
+  return hipGetLastError();
+}
+
+hipError_t f32_to_f16_rows(const float* src, int64_t n, int dim, u16* dst, hipStream_t s) {
+  const int64_t total = n * dim;
+  if (total <= 0) return hipSuccess;
+  const int blocks = (int)std::min<int64_t>((total + 255) / 256, 4096);
+  f32_to_f16_kernel<<<blocks, 256, 0, s>>>(src, total, dst);
+  return hipGetLastError();
+}
+
+}  // namespace clm

@@ -1,0 +1,229 @@
+// Exact top-k selection for the cosine search (gfx950).
+//
+// Replaces torch.topk(sims, k, largest=True, sorted=True) of
+// src/embedding/search.py:98-99 and similarity.py:57 over the score rows the
+// EPI_SCORE GEMM writes. The order is defined as (score desc, index asc):
+// CPU torch.topk leaves ties unordered (SURVEY §7 hard part 2), this fixes it.
+//
+// topk_rows: one 1024-thread workgroup per query row. Radix select on the
+// order-preserving 32-bit key of the fp32 score (digits 11/11/10 bits, LDS
+// histograms), stopping as soon as the bin holding the k-th key has <= CAP
+// members; then one collection pass gathers every key above that bin plus the
+// bin's members IN INDEX ORDER (block prefix sums, so a tie group larger than
+// CAP keeps its smallest indices), and a bitonic sort of 64-bit
+// (key, ~index) composites in LDS emits the sorted k.
+// topk_merge: sort of parts*k_in candidates per row (chunk / shard merge).
+#include "kernels.hpp"
+
+namespace clm {
+
+namespace {
+constexpr int NT = 1024;
+constexpr int CAP = 4096;
+constexpr int SORT_MAX = 8192;
+
+__device__ __forceinline__ uint32_t fkey(float f) {
+  const uint32_t u = __float_as_uint(f);
+  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+__device__ __forceinline__ float kfloat(uint32_t k) {
+  const uint32_t u = (k & 0x80000000u) ? (k & 0x7fffffffu) : ~k;
+  return __uint_as_float(u);
+}
+
+// in-place descending bitonic sort of n (power of two) u64 keys, all threads of the block
+__device__ void bitonic_desc(uint64_t* a, int n) {
+  for (int size = 2; size <= n; size <<= 1) {
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      __syncthreads();
+      for (int t = threadIdx.x; t < n / 2; t += blockDim.x) {
+        const int lo = 2 * t - (t & (stride - 1));
+        const int hi = lo + stride;
+        const bool desc = ((lo & size) == 0);
+        const uint64_t x = a[lo], y = a[hi];
+        if ((x < y) == desc) { a[lo] = y; a[hi] = x; }
+      }
+    }
+  }
+  __syncthreads();
+}
+
+__global__ __launch_bounds__(NT) void topk_rows_kernel(const float* S, int64_t lds, int64_t C, int k,
+                                                       int64_t base, float* os, int64_t* oi, int64_t ldo) {
+  __shared__ uint32_t hist[2048];
+  __shared__ uint64_t cand[SORT_MAX];
+  __shared__ uint32_t s_prefix, s_bin_cnt;
+  __shared__ int s_pbits, s_kk, s_nsure, s_nbin;
+  __shared__ int wsum[NT / 64];
+  __shared__ int lanecum[64];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int64_t row = blockIdx.x;
+  const float* s = S + row * lds;
+
+  if (tid == 0) { s_prefix = 0; s_pbits = 0; s_kk = k; }
+  __syncthreads();
+
+  // ---- radix select ---------------------------------------------------------
+  for (int pass = 0; pass < 3; ++pass) {
+    const int pbits = s_pbits;
+    const uint32_t prefix = s_prefix;
+    const int width = pass < 2 ? 11 : 10;
+    const int shift = 32 - pbits - width;
+    const int nb = 1 << width;
+    for (int i = tid; i < nb; i += NT) hist[i] = 0;
+    __syncthreads();
+    for (int64_t i = tid; i < C; i += NT) {
+      const uint32_t key = fkey(s[i]);
+      if (pbits == 0 || (key >> (32 - pbits)) == prefix) atomicAdd(&hist[(key >> shift) & (nb - 1)], 1u);
+    }
+    __syncthreads();
+    if (wid == 0) {  // find the bin (from the top) holding the kk-th key
+      const int per = nb / 64;
+      const int hi_bin = nb - 1 - lane * per;  // lane covers bins (hi_bin-per, hi_bin]
+      int gs = 0;
+      for (int q = 0; q < per; ++q) gs += hist[hi_bin - q];
+      int cum = gs;  // inclusive scan over lanes
+      for (int o = 1; o < 64; o <<= 1) {
+        const int v = __shfl_up(cum, o, 64);
+        if (lane >= o) cum += v;
+      }
+      lanecum[lane] = cum;
+      const int kk = s_kk;
+      const unsigned long long m = __ballot(cum >= kk);
+      const int first = m ? __ffsll((long long)m) - 1 : 63;
+      if (lane == first) {
+        int above = cum - gs;
+        int bin = hi_bin;
+        for (int q = 0; q < per; ++q) {
+          const int b = hi_bin - q;
+          if (above + (int)hist[b] >= kk || q == per - 1) { bin = b; break; }
+          above += hist[b];
+        }
+        s_kk = kk - above;
+        s_prefix = (prefix << width) | (uint32_t)bin;
+        s_pbits = pbits + width;
+        s_bin_cnt = hist[bin];
+      }
+    }
+    __syncthreads();
+    if (s_bin_cnt <= (uint32_t)CAP) break;
+  }
+
+  // ---- collection ------------------------------------------------------------
+  const int pbits = s_pbits;
+  const uint32_t prefix = s_prefix;
+  const int drop = 32 - pbits;
+  if (tid == 0) { s_nsure = 0; s_nbin = 0; }
+  __syncthreads();
+  uint64_t* sure = cand;            // < k entries (k <= 1024)
+  uint64_t* binb = cand + 1024;     // <= CAP entries, index order
+  for (int64_t b0 = 0; b0 < C; b0 += NT) {
+    const int64_t i = b0 + tid;
+    bool is_sure = false, is_bin = false;
+    uint32_t key = 0;
+    if (i < C) {
+      key = fkey(s[i]);
+      const uint32_t top = drop >= 32 ? 0u : (key >> drop);
+      is_sure = top > prefix;
+      is_bin = top == prefix;
+    }
+    const uint64_t comp = ((uint64_t)key << 32) | (uint64_t)(0xFFFFFFFFu - (uint32_t)i);
+    if (is_sure) sure[atomicAdd(&s_nsure, 1)] = comp;
+    const unsigned long long m = __ballot(is_bin);
+    const int rank = __popcll(m & ((1ull << lane) - 1ull));
+    if (lane == 0) wsum[wid] = __popcll(m);
+    __syncthreads();
+    int off = s_nbin;
+    for (int w = 0; w < wid; ++w) off += wsum[w];
+    if (is_bin && off + rank < CAP) binb[off + rank] = comp;
+    __syncthreads();
+    if (tid == 0) {
+      int tot = 0;
+      for (int w = 0; w < NT / 64; ++w) tot += wsum[w];
+      s_nbin = s_nbin + tot;
+    }
+    __syncthreads();
+  }
+  const int nsure = s_nsure;
+  const int nbin = min(s_nbin, CAP);
+  // compact: sure (nsure <= 1024) then bin list, pad to a power of two
+  int total = nsure + nbin;
+  int n2 = 1;
+  while (n2 < total) n2 <<= 1;
+  // move bin entries to follow the sure entries (sure region is fixed 1024)
+  // read all into registers first to avoid overlap hazards
+  uint64_t tmp[(1024 + CAP) / NT];
+#pragma unroll
+  for (int q = 0; q < (1024 + CAP) / NT; ++q) {
+    const int j = tid + q * NT;
+    uint64_t v = 0;
+    if (j < nsure) v = sure[j];
+    else if (j < total) v = binb[j - nsure];
+    tmp[q] = v;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int q = 0; q < (1024 + CAP) / NT; ++q) {
+    const int j = tid + q * NT;
+    if (j < SORT_MAX) cand[j] = tmp[q];
+  }
+  for (int j = (1024 + CAP) + tid; j < n2; j += NT) cand[j] = 0;
+  __syncthreads();
+  if (n2 > 1) bitonic_desc(cand, n2);
+  for (int j = tid; j < k; j += NT) {
+    float sc = -INFINITY;
+    int64_t ix = -1;
+    if (j < total) {
+      const uint64_t v = cand[j];
+      sc = kfloat((uint32_t)(v >> 32));
+      ix = base + (int64_t)(0xFFFFFFFFu - (uint32_t)(v & 0xFFFFFFFFu));
+    }
+    os[row * ldo + j] = sc;
+    oi[row * ldo + j] = ix;
+  }
+}
+
+__global__ __launch_bounds__(NT) void topk_merge_kernel(const float* in_s, const int64_t* in_i, int n_in,
+                                                        int k, float* os, int64_t* oi) {
+  __shared__ uint64_t cand[SORT_MAX];
+  const int64_t row = blockIdx.x;
+  int n2 = 1;
+  while (n2 < n_in) n2 <<= 1;
+  for (int j = threadIdx.x; j < n2; j += NT) {
+    uint64_t v = 0;
+    if (j < n_in) {
+      const int64_t ix = in_i[row * n_in + j];
+      if (ix >= 0)
+        v = ((uint64_t)fkey(in_s[row * n_in + j]) << 32) | (uint64_t)(0xFFFFFFFFu - (uint32_t)ix);
+    }
+    cand[j] = v;
+  }
+  __syncthreads();
+  if (n2 > 1) bitonic_desc(cand, n2);
+  for (int j = threadIdx.x; j < k; j += NT) {
+    const uint64_t v = j < n_in ? cand[j] : 0;
+    if (v == 0) { os[row * k + j] = -INFINITY; oi[row * k + j] = -1; continue; }
+    os[row * k + j] = kfloat((uint32_t)(v >> 32));
+    oi[row * k + j] = (int64_t)(0xFFFFFFFFu - (uint32_t)(v & 0xFFFFFFFFu));
+  }
+}
+}  // namespace
+
+hipError_t topk_rows(const float* scores, int64_t lds, int64_t nq, int64_t C, int k, int64_t base, float* out_s,
+                     int64_t* out_i, int64_t ldo, hipStream_t s) {
+  if (nq <= 0) return hipSuccess;
+  if (k < 1 || k > 1024 || C < 0 || C > 0xFFFFFFFFll) return hipErrorInvalidValue;
+  topk_rows_kernel<<<(unsigned)nq, NT, 0, s>>>(scores, lds, C, k, base, out_s, out_i, ldo);
+  return hipGetLastError();
+}
+
+hipError_t topk_merge(const float* in_s, const int64_t* in_i, int64_t nq, int parts, int k_in, int k,
+                      float* out_s, int64_t* out_i, hipStream_t s) {
+  if (nq <= 0) return hipSuccess;
+  const int n_in = parts * k_in;
+  if (n_in > SORT_MAX || k < 1 || k > 1024) return hipErrorInvalidValue;
+  topk_merge_kernel<<<(unsigned)nq, NT, 0, s>>>(in_s, in_i, n_in, k, out_s, out_i);
+  return hipGetLastError();
+}
+
+}  // namespace clm

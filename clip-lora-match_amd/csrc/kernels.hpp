@@ -1,0 +1,90 @@
+// Host-callable launchers of the gfx950 kernels in k_*.hip.
+#pragma once
+#include "clm_common.hpp"
+
+namespace clm {
+
+// ---------------------------------------------------------------- GEMM ------
+// C[M,N] = A[M,K] . W[N,K]^T  (both operands K-contiguous, nn.Linear layout),
+// bf16 or fp16 operands, fp32 accumulate, fused epilogue. K % 64 == 0.
+enum Epi {
+  EPI_STORE = 0,  // out16[m,n] = acc + bias[n]
+  EPI_GELU = 1,   // out16[m,n] = quick_gelu(acc + bias[n])
+  EPI_RESID = 2,  // outf[m,n] += acc + bias[n]            (fp32 residual stream)
+  EPI_PATCH = 3,  // outf[b*(G+1)+1+p, n] = acc + aux[(1+p)*aux_ld + n], m = b*G+p
+  EPI_SCORE = 4   // outf[m,n] = acc * rscale[m] * cscale[n]  (cosine scores)
+};
+
+struct GemmArgs {
+  const u16* A; int64_t lda;
+  const u16* W; int64_t ldw;
+  int M, N, K;
+  void* out; int64_t ldo;
+  const float* bias;
+  const float* aux; int64_t aux_ld; int group;
+  const float* rscale; const float* cscale;
+};
+
+hipError_t gemm(bool bf16, int epi, const GemmArgs& g, hipStream_t s);
+
+// ----------------------------------------------------------- row ops -------
+// LayerNorm over rows of a fp32 matrix, one wave per row.
+//   mode 0: x = src rows                         (src = h)
+//   mode 1: x = tok[ids[r]] + pos[r % L]         (text embedding gather), h written
+// If g2 != null: h_out = LN(x; g1,b1) is written to hf (fp32) and y = LN(h_out; g2,b2)
+// else: (mode 1 writes hf = x) y = LN(x; g1,b1).
+// y (compute dtype) gets row stride ldy; if loraA != null, the r_ext LoRA
+// down-projections of the fp32 LN output are appended at y[:, d : d+r_pad).
+struct LnArgs {
+  int mode;
+  const float* src; int64_t lds;       // mode 0 source rows
+  const int32_t* ids; const float* tok; const float* pos; int L;   // mode 1
+  float* hf; int64_t ldh;              // fp32 output rows (may alias src)
+  const float* g1; const float* b1;
+  const float* g2; const float* b2;
+  u16* y; int64_t ldy;
+  const float* loraA; int r_ext; int r_pad;   // [r_ext, d] fp32
+  int M, d; float eps;
+};
+hipError_t layernorm(bool bf16, const LnArgs& a, hipStream_t s);
+
+// y[:, K : K+r_pad) = (X[:, :K] . A^T) for LoRA K-extension of a GEMM whose input
+// is not a LayerNorm output (out_proj after attention, fc2 after GELU).
+hipError_t lora_down(bool bf16, u16* X, int64_t ldx, int M, int K, const float* A, int r_ext,
+                     int r_pad, hipStream_t s);
+
+// patchify + (u8 rescale/normalise via lut | f32 copy) -> P[B*G*G, Kp] (compute dtype)
+hipError_t patchify(bool bf16, const void* pix, int layout, int B, int S, int p, int C,
+                    const float* lut /*[C*256]*/, u16* P, int Kp, hipStream_t s);
+
+// h[b*T + 0, :] = cls + pos[0]
+hipError_t write_cls(float* h, int64_t ldh, int B, int T, int d, const float* cls,
+                     const float* pos, hipStream_t s);
+
+// pooled row -> LN -> projection (fp32, projT [d, D]) -> optional L2 norm -> out
+//   ids == null: row b*T (CLS); else row b*T + (first eos in ids[b]) (argmax if eos==2)
+hipError_t pool_project(const float* h, int64_t ldh, int B, int T, int d, const int32_t* ids,
+                        int eos, const float* g, const float* bta, float eps, const float* projT,
+                        int D, void* out, int out_dtype, int normalize, hipStream_t s);
+
+// ----------------------------------------------------------- attention -----
+// qkv [B*T, 3d] (q pre-scaled by head_dim^-0.5), out [B*T, ldo] compute dtype.
+hipError_t attention(bool bf16, bool causal, const u16* qkv, int64_t ldq, u16* out, int64_t ldo,
+                     int B, int T, int H, int d, hipStream_t s);
+
+// ----------------------------------------------------------- search --------
+// rows f32|f16 [n, dim] -> fp16 dst + fp32 inverse norms of the fp16-rounded rows
+// (norm_src = 0) or of the source rows (norm_src = 1)
+hipError_t rows_to_f16(const void* src, int src_dtype, int64_t n, int dim, u16* dst,
+                       float* inv_norm, hipStream_t s, int norm_src);
+// per-row top-k over scores [nq, C] (row stride lds): out sorted by (score desc,
+// idx asc); idx = base + column.
+hipError_t topk_rows(const float* scores, int64_t lds, int64_t nq, int64_t C, int k,
+                     int64_t base, float* out_s, int64_t* out_i, int64_t ldo, hipStream_t s);
+// merge `parts` candidate lists per row: in [nq, parts*k_in] -> out [nq, k]
+hipError_t topk_merge(const float* in_s, const int64_t* in_i, int64_t nq, int parts, int k_in,
+                      int k, float* out_s, int64_t* out_i, hipStream_t s);
+hipError_t l2_normalize_rows(float* rows, int64_t n, int dim, hipStream_t s);
+hipError_t f32_to_f16_rows(const float* src, int64_t n, int dim, u16* dst, hipStream_t s);
+
+}  // namespace clm

@@ -1,0 +1,219 @@
+"""Drop-in for src/embedding/search.py: SearchResult + TextSearchIndex, backed by
+an HBM-resident fp16 index (libclm clm_index_*) and the gfx950 cosine GEMM +
+exact top-k kernels.
+
+  SearchResult                       search.py:14-20
+  TextSearchIndex.__init__           search.py:24-68  (key variants :41-56, re-normalise :68)
+  .search_with_embedding             search.py:70-115 (shape checks :80-90, safe metadata :103-105)
+  .search_by_text / .search_by_image search.py:117-151
+New: .append / .save keep the index resident with O(1)
+append instead of FinderService's torch.cat + full re-save per report
+(finder_service.py:93-103,172-185), and .search_batch serves many queries per
+launch.
+
+Top-k order is (score desc, index asc); CPU torch.topk leaves exact ties in
+arbitrary order (SURVEY §7 hard part 2).
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass
+from pathlib import Path
+from typing import List, Optional, Sequence, Tuple, Union
+
+import numpy as np
+import torch
+
+from . import _capi as C
+
+
+@dataclass
+class SearchResult:
+    """Satu hasil pencarian."""
+    index: int
+    score: float
+    image_path: str
+    text: str
+
+
+def _pad_dim(x: torch.Tensor, dim_p: int) -> torch.Tensor:
+    if x.shape[-1] == dim_p:
+        return x
+    return torch.nn.functional.pad(x, (0, dim_p - x.shape[-1]))
+
+
+class CosineIndex:
+    """GPU index of fp16 rows + fp32 inverse norms (score = q.row / (|q| |row|))."""
+
+    def __init__(self, dim: int, capacity: int = 1024, device=None):
+        C.require_gpu()
+        self.dim = int(dim)
+        self.dim_p = (self.dim + 63) // 64 * 64          # GEMM K granule; zero padding keeps dots/norms
+        self.device = torch.device("cuda", torch.cuda.current_device() if device is None
+                                   else (torch.device(device).index or 0))
+        h = ctypes.c_void_p()
+        C.check(C.lib().clm_index_create(self.device.index, max(int(capacity), 1), self.dim_p, ctypes.byref(h)),
+                "clm_index_create")
+        self._h = h
+
+    def __len__(self) -> int:
+        return int(C.lib().clm_index_size(self._h))
+
+    def append(self, rows) -> None:
+        t = torch.as_tensor(rows)
+        if t.dim() == 1:
+            t = t.unsqueeze(0)
+        if t.dim() != 2 or t.shape[1] != self.dim:
+            raise ValueError(f"rows must be [n, {self.dim}], got {tuple(t.shape)}")
+        if t.dtype not in (torch.float32, torch.float16):
+            t = t.float()
+        t = _pad_dim(t.to(self.device), self.dim_p).contiguous()
+        code = C.CLM_F32 if t.dtype == torch.float32 else C.CLM_F16
+        C.check(C.lib().clm_index_append(self._h, C.ptr(t), code, t.shape[0], C.stream_of(self.device)),
+                "clm_index_append")
+
+    def reset(self) -> None:
+        C.check(C.lib().clm_index_reset(self._h))
+
+    def set_offset(self, offset: int) -> None:
+        C.check(C.lib().clm_index_set_offset(self._h, int(offset)))
+
+    def read(self, start: int = 0, n: Optional[int] = None) -> torch.Tensor:
+        n = len(self) - start if n is None else n
+        out = torch.empty((n, self.dim_p), dtype=torch.float32)
+        C.check(C.lib().clm_index_read(self._h, start, n, C.ptr(out), C.stream_of(self.device)), "clm_index_read")
+        return out[:, :self.dim]
+
+    def search(self, queries, k: int) -> Tuple[torch.Tensor, torch.Tensor]:
+        """queries [nq, dim] (f32/f16, any device) -> (scores [nq,k] f32, idx [nq,k] i64) on the GPU."""
+        q = torch.as_tensor(queries)
+        if q.dim() == 1:
+            q = q.unsqueeze(0)
+        if q.dim() != 2 or q.shape[1] != self.dim:
+            raise ValueError(f"queries must be [nq, {self.dim}], got {tuple(q.shape)}")
+        if q.dtype not in (torch.float32, torch.float16):
+            q = q.float()
+        q = _pad_dim(q.to(self.device), self.dim_p).contiguous()
+        nq = q.shape[0]
+        s = torch.empty((nq, k), dtype=torch.float32, device=self.device)
+        i = torch.empty((nq, k), dtype=torch.int64, device=self.device)
+        code = C.CLM_F32 if q.dtype == torch.float32 else C.CLM_F16
+        C.check(C.lib().clm_index_search(self._h, C.ptr(q), code, nq, int(k), C.ptr(s), C.ptr(i),
+                                         C.stream_of(self.device)), "clm_index_search")
+        return s, i
+
+    def close(self) -> None:
+        if getattr(self, "_h", None):
+            C.lib().clm_index_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class TextSearchIndex:
+    def __init__(self, index_path: Union[str, Path, None] = None, *, embeddings=None, image_paths=None,
+                 texts=None, device=None):
+        if index_path is not None:
+            index_path = Path(index_path)
+            if not index_path.exists():
+                raise FileNotFoundError(f"Index file not found: {index_path}")
+            obj = torch.load(index_path, map_location="cpu", weights_only=True)
+        else:
+            obj = {"embeddings": embeddings, "image_paths": image_paths, "texts": texts}
+
+        embs = obj.get("embeddings")
+        if embs is None:
+            raise ValueError("Index file does not contain 'embeddings'")
+        self.embeddings: torch.Tensor = torch.as_tensor(embs).float().cpu()
+        if self.embeddings.dim() == 1:
+            self.embeddings = self.embeddings.unsqueeze(0)
+
+        images = obj.get("image_paths")
+        if images is None:
+            images = obj.get("image_path")
+        if images is None:
+            images = []
+        self.image_paths: list = list(images)
+
+        texts_ = obj.get("texts")
+        if texts_ is None:
+            texts_ = obj.get("text")
+        if texts_ is None:
+            texts_ = []
+        self.texts: list = list(texts_)
+
+        if self.embeddings.size(0) != len(self.image_paths):
+            print(f"[TextSearchIndex] WARNING: embeddings rows ({self.embeddings.size(0)}) "
+                  f"!= len(image_paths) ({len(self.image_paths)})")
+
+        self.num_items, self.dim = self.embeddings.shape
+        print(f"[TextSearchIndex] Loaded {self.num_items} items with dim={self.dim}")
+
+        # Pastikan normalized (search.py:68) -- fp32 on the host, as the reference does
+        self.embeddings = self.embeddings / self.embeddings.norm(dim=-1, keepdim=True)
+        self._gpu = CosineIndex(self.dim, capacity=max(self.num_items, 1024), device=device)
+        if self.num_items:
+            self._gpu.append(self.embeddings)
+
+    # --------------------------------------------------------------- search --
+    def search_batch(self, queries, top_k: int = 5) -> Tuple[torch.Tensor, torch.Tensor]:
+        """[nq, d] queries -> (scores [nq, k], indices [nq, k]) on the GPU, k = min(top_k, num_items)."""
+        k = min(int(top_k), self.num_items)
+        if k < 0:
+            raise RuntimeError("selected index k out of range")
+        if k == 0:
+            q = torch.as_tensor(queries)
+            nq = 1 if q.dim() == 1 else q.shape[0]
+            return torch.empty((nq, 0)), torch.empty((nq, 0), dtype=torch.int64)
+        if k > 1024:
+            raise ValueError("top_k > 1024 is not supported by the GPU top-k kernel")
+        return self._gpu.search(queries, k)
+
+    def search_with_embedding(self, query_emb: torch.Tensor, top_k: int = 5) -> List[SearchResult]:
+        """query_emb: shape (d,) atau (1, d)."""
+        query_emb = torch.as_tensor(query_emb)
+        if query_emb.ndim == 1:
+            query_emb = query_emb.unsqueeze(0)
+        elif query_emb.ndim != 2 or query_emb.shape[0] != 1:
+            raise ValueError(f"query_emb must be shape (d,) or (1, d), got {tuple(query_emb.shape)}")
+        if query_emb.shape[-1] != self.dim:
+            raise ValueError(f"query_emb dim {query_emb.shape[-1]} != index dim {self.dim}")
+        scores, indices = self.search_batch(query_emb, top_k)
+        results: List[SearchResult] = []
+        for idx, score in zip(indices[0].tolist(), scores[0].tolist()):
+            img = self.image_paths[idx] if idx < len(self.image_paths) else ""
+            txt = self.texts[idx] if idx < len(self.texts) else ""
+            results.append(SearchResult(index=idx, score=float(score), image_path=img, text=txt))
+        return results
+
+    def search_by_text(self, query, model, processor, device, top_k: int = 5) -> List[SearchResult]:
+        from .clip_model import encode_text
+        return self.search_with_embedding(encode_text(query, model, processor, device), top_k=top_k)
+
+    def search_by_image(self, image_path, model, processor, device, top_k: int = 5) -> List[SearchResult]:
+        from .clip_model import encode_image
+        return self.search_with_embedding(encode_image(image_path, model, processor, device), top_k=top_k)
+
+    # ------------------------------------------------------- resident append --
+    def append(self, embeddings, image_paths: Sequence[str] = (), texts: Sequence[str] = ()) -> None:
+        e = torch.as_tensor(embeddings).float().cpu()
+        if e.dim() == 1:
+            e = e.unsqueeze(0)
+        if e.shape[1] != self.dim:
+            raise ValueError(f"embedding dim {e.shape[1]} != index dim {self.dim}")
+        e = e / e.norm(dim=-1, keepdim=True)
+        self._gpu.append(e)
+        self.embeddings = torch.cat([self.embeddings, e], dim=0)
+        self.image_paths.extend(image_paths)
+        self.texts.extend(texts)
+        self.num_items = self.embeddings.shape[0]
+
+    def save(self, path: Union[str, Path]) -> None:
+        path = Path(path)
+        path.parent.mkdir(parents=True, exist_ok=True)
+        torch.save({"embeddings": self.embeddings, "image_paths": list(self.image_paths),
+                    "texts": list(self.texts)}, path)

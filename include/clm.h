@@ -1,0 +1,159 @@
+/*
+ * clm.h -- C-ABI of libclm.so, the MI355X (gfx950) CLIP+LoRA encode and
+ * cosine top-k library. Plain pointers and sizes only; no torch types.
+ *
+ * Each entry point replaces one reference interface (file:line into
+ * youngalip/clip-lora-match, /root/reference):
+ *
+ *   clm_ctx_create/_destroy   models/clip_model.py:37-82  load_clip_model
+ *                              (device/dtype from _get_device :23-28, _get_dtype :31-34)
+ *   clm_load_tensor            CLIPModel.from_pretrained (clip_model.py:59) and
+ *                              PeftModel.from_pretrained (clip_model.py:78): tensors by
+ *                              their transformers / PEFT state-dict names
+ *   clm_finalize               model.eval() (clip_model.py:81): fuse q/k/v, merge or
+ *                              pack LoRA (models/lora_adapter.py:21-43 scaling alpha/r)
+ *   clm_encode_image           encode_image clip_model.py:89-118,
+ *                              embed_images_batch src/embedding/embed_image.py:57-98
+ *   clm_encode_text            encode_text clip_model.py:121-150,
+ *                              embed_text src/embedding/embed_text.py:11-60
+ *   clm_index_create/_append   TextSearchIndex.__init__ src/embedding/search.py:24-68
+ *                              (rows re-normalised at load, :68)
+ *   clm_index_search           TextSearchIndex.search_with_embedding search.py:70-115,
+ *                              top_k_similar src/embedding/similarity.py:36-58
+ *   clm_cosine_scores          cosine_similarity similarity.py:10-33
+ *   clm_topk_merge             (new) merge of per-shard top-k lists for the
+ *                              8-GPU sharded search
+ *   clm_l2_normalize           v / ||v||_2 (clip_model.py:116,148; search.py:68,93)
+ *
+ * Conventions
+ *   - return 0 (CLM_OK) on success, a negative CLM_E_* code on error;
+ *     clm_last_error() returns a thread-local message for the last failure.
+ *   - pointers may be device (hipMalloc / torch cuda) or host memory; host
+ *     buffers are staged through the context's device workspace.
+ *   - `stream` is a hipStream_t (NULL = the legacy default stream). Calls are
+ *     asynchronous w.r.t. the host only when every buffer is device memory.
+ *   - one context per device; calls on one context must be externally
+ *     serialised; different contexts are independent.
+ */
+#ifndef CLM_H
+#define CLM_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum {
+  CLM_OK = 0,
+  CLM_E_ARG = -1,     /* bad argument / shape (Python: ValueError)         */
+  CLM_E_OOM = -2,     /* device allocation failed                          */
+  CLM_E_HIP = -3,     /* HIP runtime error                                 */
+  CLM_E_STATE = -4,   /* call out of order (e.g. encode before finalize)   */
+  CLM_E_MISSING = -5  /* a required tensor was never loaded                */
+};
+
+enum { CLM_F32 = 0, CLM_F16 = 1, CLM_BF16 = 2, CLM_U8 = 3, CLM_I32 = 4, CLM_I64 = 5 };
+
+/* pixel layouts for clm_encode_image */
+enum {
+  CLM_PIX_U8_HWC = 0,  /* raw uint8 [n, S, S, 3]; rescale+normalise fused in-kernel */
+  CLM_PIX_F32_CHW = 1  /* CLIPProcessor pixel_values float32 [n, 3, S, S]          */
+};
+
+/* LoRA target bits (PEFT target_modules, lora_config.yaml:3-7) */
+enum {
+  CLM_LORA_Q = 1, CLM_LORA_K = 2, CLM_LORA_V = 4, CLM_LORA_OUT = 8,
+  CLM_LORA_FC1 = 16, CLM_LORA_FC2 = 32
+};
+
+enum { CLM_LORA_MERGED = 0, CLM_LORA_UNMERGED = 1 };
+
+typedef struct clm_ctx clm_ctx;
+typedef struct clm_index clm_index;
+
+typedef struct {
+  int32_t hidden, layers, heads, mlp;
+} clm_tower_desc;
+
+typedef struct {
+  clm_tower_desc vision, text;
+  int32_t patch, image_size, channels;
+  int32_t vocab, max_pos, proj_dim;
+  int32_t eos_token_id;       /* 2 selects the legacy argmax(ids) pooling rule */
+  float ln_eps;
+  int32_t lora_r;             /* 0 = no LoRA */
+  float lora_alpha;
+  uint32_t lora_targets;      /* CLM_LORA_* bitmask */
+  int32_t lora_mode;          /* CLM_LORA_MERGED | CLM_LORA_UNMERGED (K-extension) */
+  int32_t compute_dtype;      /* CLM_BF16 | CLM_F16: GEMM/attention operand type */
+  int32_t max_batch;          /* workspace is sized for this many images/captions */
+  float mean[3], std[3];      /* preprocess.normalize (clip_config.yaml:10-12) */
+} clm_model_desc;
+
+int clm_ctx_create(int hip_device, const clm_model_desc* desc, clm_ctx** out);
+int clm_ctx_destroy(clm_ctx* ctx);
+
+/* host tensor by transformers/PEFT name; dtype CLM_F32|CLM_F16|CLM_BF16.
+ * Copied (as float32) into the context; device upload happens in finalize. */
+int clm_load_tensor(clm_ctx* ctx, const char* name, const void* host_ptr, int dtype,
+                    const int64_t* shape, int ndim);
+int clm_finalize(clm_ctx* ctx);
+/* drop all LoRA tensors and re-finalize as the base model */
+int clm_set_lora_enabled(clm_ctx* ctx, int enabled);
+
+/* n images -> out [n, proj_dim] (CLM_F32 or CLM_F16); normalize != 0 => unit rows */
+int clm_encode_image(clm_ctx* ctx, const void* pixels, int pix_layout, int n, void* out,
+                     int out_dtype, int normalize, void* stream);
+/* ids int32 [n, L] (L <= max_pos; each row holds an EOS) -> out [n, proj_dim] */
+int clm_encode_text(clm_ctx* ctx, const int32_t* ids, int n, int L, void* out, int out_dtype,
+                    int normalize, void* stream);
+
+/* GPU-resident index of fp16 rows + fp32 inverse norms (score = q . row / ||row||) */
+int clm_index_create(int hip_device, int64_t capacity, int dim, clm_index** out);
+int clm_index_destroy(clm_index* idx);
+/* rows [n, dim] CLM_F32|CLM_F16, host or device; stored fp16, inv-norm of the
+ * fp16-rounded row in fp32 */
+int clm_index_append(clm_index* idx, const void* rows, int dtype, int64_t n, void* stream);
+int64_t clm_index_size(const clm_index* idx);
+int clm_index_reset(clm_index* idx);
+/* index of row 0 in the global (all-shard) numbering, for multi-GPU shards */
+int clm_index_set_offset(clm_index* idx, int64_t global_offset);
+/* copy rows [start, start+n) back as fp32 (host or device dst) */
+int clm_index_read(clm_index* idx, int64_t start, int64_t n, float* dst, void* stream);
+/* q [nq, dim] CLM_F32|CLM_F16 (normalised in-kernel); k in [1, 1024];
+ * out_scores [nq, k] f32, out_idx [nq, k] i64; order: score desc, index asc;
+ * slots past the index size are filled with (-inf, -1). */
+int clm_index_search(clm_index* idx, const void* q, int q_dtype, int64_t nq, int k,
+                     float* out_scores, int64_t* out_idx, void* stream);
+
+/* full cosine matrix: out [nq, n] f32 = normalise(q) . normalise(c)^T */
+int clm_cosine_scores(int hip_device, const float* q, int64_t nq, const float* c, int64_t n,
+                      int dim, float* out, void* stream);
+
+/* merge `parts` sorted candidate lists per query: scores/idx [nq, parts*k_in]
+ * -> [nq, k] by (score desc, index asc) */
+int clm_topk_merge(int hip_device, const float* scores, const int64_t* idx, int64_t nq,
+                   int parts, int k_in, int k, float* out_scores, int64_t* out_idx, void* stream);
+
+/* rows [n, dim] f32 in place (device or host) */
+int clm_l2_normalize(int hip_device, float* rows, int64_t n, int dim, void* stream);
+
+/* Kernel timing by category, measured with hipEvents recorded on the launch
+ * stream around every kernel of clm_encode_* while enabled (adds event
+ * overhead; keep it off in timed regions). categories: CLM_PROF_* */
+enum { CLM_PROF_GEMM = 0, CLM_PROF_ATTN = 1, CLM_PROF_LN = 2, CLM_PROF_OTHER = 3, CLM_PROF_NCAT = 4 };
+int clm_prof_enable(clm_ctx* ctx, int enable);   /* enabling also resets the counters */
+/* sums since enable: kernel milliseconds, algorithmic FLOPs (GEMM/ATTN) or
+ * algorithmic bytes (LN/OTHER), and launch count, for one category */
+int clm_prof_read(clm_ctx* ctx, int category, double* ms, double* work, int64_t* launches);
+
+const char* clm_last_error(void);
+const char* clm_version(void);
+/* sizeof(clm_model_desc), so bindings can verify their struct layout */
+int32_t clm_model_desc_size(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* CLM_H */

@@ -1,0 +1,123 @@
+"""Generate the golden fixtures in tests/golden/ (run in the build container, where
+transformers 5.15.0 and the read-only reference at /root/reference exist):
+
+  python tests/golden/make_golden.py
+
+Encoder goldens: transformers.CLIPModel fp32 on CPU (the arithmetic the
+reference's models/clip_model.py delegates to, clip_model.py:59,115,144) with
+the deterministic synthetic weights of weights.synthetic_state_dict, PEFT LoRA
+restated as forward hooks y += (alpha/r) (x A^T) B^T on every targeted Linear
+(PEFT matches target_modules by suffix: both towers), `.pooler_output` (the
+transformers>=5 spelling of what get_*_features returned in 4.x)
+and the L2 normalisation of clip_model.py:116,148. Pixel values come from
+transformers' CLIPImageProcessor on the synthetic uint8 images.
+
+Search goldens: the reference's own src/embedding/similarity.py top_k_similar
+(imported from /root/reference; it needs only torch) on synthetic normalised
+Gaussian fp16-rounded rows/queries, and on the reference's committed
+data/index/custom_items_index.pt (copied here as a data fixture).
+
+Only inputs' seeds and outputs are stored; the weights are regenerated from
+their seeds by the tests.
+"""
+from __future__ import annotations
+
+import importlib.util
+import os
+import shutil
+import sys
+
+import numpy as np
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, REPO)
+REF = "/root/reference"
+
+import clip_lora_match_amd as clm  # noqa: E402
+from clip_lora_match_amd import synthetic as syn  # noqa: E402
+from clip_lora_match_amd import weights as W  # noqa: E402
+from oracle import hf_ref as H  # noqa: E402
+
+torch.set_num_threads(8)
+
+
+def encode(cfg, sd, lora, images, ids):
+    m = H.hf_model(cfg, sd, lora)
+    return H.encode(m, cfg, H.pixel_values(cfg, images), ids)
+
+
+def encoder_golden(name, preset, n_img, n_txt, L, lora_on, img_seed=1234, cap_seed=99):
+    cfg = clm.get_preset(preset)
+    if not lora_on:
+        cfg = cfg.with_lora(0, 0.0, ())
+    sd = W.synthetic_state_dict(cfg, 0)
+    lora = W.synthetic_lora(cfg, 1) if lora_on else None
+    images = syn.images_u8(n_img, cfg.image_size, img_seed)
+    ids = syn.captions(n_txt, L, cfg.bos_token_id, cfg.eos_token_id, cap_seed)
+    fi, ft = encode(cfg, sd, lora, images, ids)
+    out = dict(preset=np.array(preset), lora=np.array(int(lora_on)), r=np.array(cfg.lora_r),
+               alpha=np.array(cfg.lora_alpha), targets=np.array(",".join(cfg.lora_targets)),
+               weight_seed=np.array(0), lora_seed=np.array(1), img_seed=np.array(img_seed),
+               cap_seed=np.array(cap_seed), n_img=np.array(n_img), n_txt=np.array(n_txt), L=np.array(L),
+               ids=ids, emb_img=fi, emb_txt=ft)
+    if lora_on:  # also the base model, so tests can prove LoRA changes the result
+        fi0, ft0 = encode(cfg, sd, None, images, ids)
+        out.update(emb_img_base=fi0, emb_txt_base=ft0)
+    np.savez_compressed(os.path.join(HERE, name), **out)
+    print(f"{name}: img {fi.shape} txt {ft.shape}")
+
+
+def _load_ref_similarity():
+    spec = importlib.util.spec_from_file_location("ref_similarity", os.path.join(REF, "src/embedding/similarity.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
+def search_golden():
+    sim = _load_ref_similarity()
+    n, nq, dim = 4096, 64, 512
+    rows = syn.gaussian_rows(n, dim, seed=7, fp16=True)
+    qs = syn.gaussian_rows(nq, dim, seed=8, fp16=True)
+    E = torch.from_numpy(rows.astype(np.float32))
+    out = dict(n=np.array(n), nq=np.array(nq), dim=np.array(dim), row_seed=np.array(7), q_seed=np.array(8))
+    for k in (1, 5, 10, 50):
+        vals = np.zeros((nq, k), np.float32)
+        idx = np.zeros((nq, k), np.int64)
+        for i in range(nq):
+            v, ix = sim.top_k_similar(torch.from_numpy(qs[i].astype(np.float32)), E, k)
+            vals[i], idx[i] = v.numpy(), ix.numpy()
+        out[f"vals_k{k}"] = vals
+        out[f"idx_k{k}"] = idx
+    cs = sim.cosine_similarity(torch.from_numpy(qs[0].astype(np.float32)), E).numpy()
+    out["cos_q0"] = cs.astype(np.float32)
+    np.savez_compressed(os.path.join(HERE, "search_gauss.npz"), **out)
+    print("search_gauss.npz")
+
+    # the reference's committed 6x512 index (data fixture) + self-query top-3
+    src = os.path.join(REF, "data/index/custom_items_index.pt")
+    dst = os.path.join(HERE, "custom_items_index.pt")
+    shutil.copyfile(src, dst)
+    obj = torch.load(dst, map_location="cpu", weights_only=True)
+    Ec = obj["embeddings"].float()
+    vals = np.zeros((Ec.shape[0], 3), np.float32)
+    idx = np.zeros((Ec.shape[0], 3), np.int64)
+    for i in range(Ec.shape[0]):
+        v, ix = sim.top_k_similar(Ec[i], Ec, 3)
+        vals[i], idx[i] = v.numpy(), ix.numpy()
+    np.savez_compressed(os.path.join(HERE, "custom_index_top3.npz"), vals=vals, idx=idx)
+    print("custom_index_top3.npz", idx.tolist())
+
+
+if __name__ == "__main__":
+    which = sys.argv[1:] or ["tiny", "b32", "l14", "search"]
+    if "tiny" in which:
+        encoder_golden("enc_tiny_lora.npz", "tiny", 4, 4, 16, True)
+    if "b32" in which:
+        encoder_golden("enc_b32_lora.npz", "ViT-B/32", 4, 4, 77, True)
+    if "l14" in which:
+        encoder_golden("enc_l14_lora.npz", "ViT-L/14@336", 2, 2, 77, True)
+    if "search" in which:
+        search_golden()
