@@ -48,6 +48,10 @@ def lib():
     global _lib
     if _lib is not None:
         return _lib
+    # PyTorch-ROCm ships its own libamdhip64 (SONAME libamdhip64.so.7). Loading torch first
+    # makes libclm's DT_NEEDED bind to that same runtime, so torch streams and device
+    # pointers are native objects of the runtime libclm calls (one HIP runtime per process).
+    import torch  # noqa: F401
     if not os.path.exists(LIB_PATH):
         raise ImportError(
             f"libclm.so not found at {LIB_PATH}: build it with `make -C clip-lora-match_amd/csrc` "
@@ -77,6 +81,10 @@ def lib():
         "clm_version": (c_char_p, []),
         "clm_model_desc_size": (c_int32, []),
         "clm_prof_enable": (c_int, [c_void_p, c_int]),
+        "clm_gemm": (c_int, [c_int, c_int, c_int, c_int, c_void_p, c_int64, c_void_p, c_int64, c_int, c_int, c_int,
+                             c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_void_p]),
+        "clm_gemm_num_configs": (c_int, []),
+        "clm_attention": (c_int, [c_int, c_int, c_int, c_void_p, c_void_p, c_int64, c_int, c_int, c_int, c_void_p]),
         "clm_prof_read": (c_int, [c_void_p, c_int, POINTER(ctypes.c_double), POINTER(ctypes.c_double),
                                   POINTER(c_int64)]),
     }
@@ -93,8 +101,10 @@ EXPORTED = (
     "clm_encode_image", "clm_encode_text", "clm_index_create", "clm_index_destroy", "clm_index_append",
     "clm_index_size", "clm_index_reset", "clm_index_set_offset", "clm_index_read", "clm_index_search",
     "clm_cosine_scores", "clm_topk_merge", "clm_l2_normalize", "clm_last_error", "clm_version",
-    "clm_model_desc_size", "clm_prof_enable", "clm_prof_read",
+    "clm_model_desc_size", "clm_prof_enable", "clm_prof_read", "clm_gemm", "clm_gemm_num_configs",
+    "clm_attention",
 )
+CLM_EPI_STORE, CLM_EPI_GELU, CLM_EPI_RESID, CLM_EPI_SCORE = 0, 1, 2, 4
 CLM_PROF_GEMM, CLM_PROF_ATTN, CLM_PROF_LN, CLM_PROF_OTHER = 0, 1, 2, 3
 
 

@@ -557,6 +557,36 @@ const char* clm_last_error(void) { return g_err.c_str(); }
 const char* clm_version(void) { return "clm 0.1.0 gfx950"; }
 int32_t clm_model_desc_size(void) { return (int32_t)sizeof(clm_model_desc); }
 
+int clm_gemm(int hip_device, int dtype, int epilogue, int config, const void* A, int64_t lda, const void* W,
+             int64_t ldw, int M, int N, int K, void* out, int64_t ldo, const float* bias, const float* rscale,
+             const float* cscale, void* stream) {
+  if (dtype != CLM_BF16 && dtype != CLM_F16) return fail(CLM_E_ARG, "dtype must be bf16 or f16");
+  if (epilogue != EPI_STORE && epilogue != EPI_GELU && epilogue != EPI_RESID && epilogue != EPI_SCORE)
+    return fail(CLM_E_ARG, "bad epilogue");
+  if (config >= gemm_num_configs()) return fail(CLM_E_ARG, "bad config");
+  if (M < 0 || N < 0 || K <= 0 || K % 64) return fail(CLM_E_ARG, "bad shape (K % 64 == 0)");
+  DeviceGuard g(hip_device);
+  GemmArgs a{};
+  a.A = (const u16*)A; a.lda = lda; a.W = (const u16*)W; a.ldw = ldw; a.M = M; a.N = N; a.K = K;
+  a.out = out; a.ldo = ldo; a.bias = bias; a.rscale = rscale; a.cscale = cscale;
+  hipError_t e = gemm_cfg(dtype == CLM_BF16, epilogue, config, a, (hipStream_t)stream);
+  if (e != hipSuccess) return fail(CLM_E_HIP, std::string("gemm: ") + hipGetErrorString(e));
+  return CLM_OK;
+}
+
+int clm_gemm_num_configs(void) { return gemm_num_configs(); }
+
+int clm_attention(int hip_device, int dtype, int causal, const void* qkv, void* out, int64_t ldo, int B, int T,
+                  int H, void* stream) {
+  if (dtype != CLM_BF16 && dtype != CLM_F16) return fail(CLM_E_ARG, "dtype must be bf16 or f16");
+  if (B < 0 || T < 0 || H <= 0) return fail(CLM_E_ARG, "bad shape");
+  DeviceGuard g(hip_device);
+  hipError_t e = attention(dtype == CLM_BF16, causal != 0, (const u16*)qkv, 3LL * H * 64, (u16*)out, ldo, B, T, H,
+                           H * 64, (hipStream_t)stream);
+  if (e != hipSuccess) return fail(CLM_E_HIP, std::string("attention: ") + hipGetErrorString(e));
+  return CLM_OK;
+}
+
 int clm_prof_enable(clm_ctx* ctx, int enable) {
   if (!ctx) return fail(CLM_E_ARG, "null ctx");
   DeviceGuard g(ctx->dev);

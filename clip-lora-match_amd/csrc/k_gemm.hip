@@ -7,151 +7,279 @@
 // bias, quick-GELU, residual-add, positional-embedding and cosine-scaling
 // epilogues fused.
 //
-// Tile 128x128x64, 256 threads = 4 waves (2x2), each wave 64x64 = 4x4 blocks of
-// v_mfma_f32_16x16x32_{bf16,f16}. Both operand tiles are staged HBM/L2 -> LDS
-// by global_load_lds_dwordx4 (16 B per lane, lane-linear LDS image), with the
-// XOR chunk swizzle applied to the per-lane SOURCE address so fragment reads
-// (ds_read_b128, 16 rows per lane group) are bank-conflict free. Two LDS
-// stages: tile k+1 streams in while tile k feeds the MFMAs. Workgroup ids are
-// remapped XCD-aware so the N-tiles sharing one A row-panel run on one XCD.
+// Structure (templated tile BM x BN x 64, WM x WN waves, STAGES-deep LDS ring):
+//  * both operand tiles stream HBM/L2 -> LDS by global_load_lds_dwordx4 (16 B per
+//    lane, lane-linear 1 KiB per wave-instruction = 8 rows of 128 B); the XOR chunk
+//    swizzle is applied to the per-lane SOURCE address so that the ds_read_b128
+//    fragment reads (16 rows per lane group) are bank-conflict free;
+//  * STAGES = 3: two K-tiles stay in flight across the (raw) barrier, retired by a
+//    counted s_waitcnt vmcnt(L) -- never vmcnt(0) in the steady state;
+//  * operands are SWAPPED in the MFMA (W rows feed the A port): the 16x16 C-block
+//    then has the output row m on the lane and 4 consecutive output columns in the
+//    lane's 4 accumulator registers, so every epilogue access is a 4-wide vector
+//    (8 B bf16 / 16 B fp32) instead of 2-byte scatter;
+//  * workgroup ids are remapped XCD-aware so the N-tiles sharing one A row-panel
+//    (and its L2 lines) run on one XCD.
 #include "kernels.hpp"
 
 namespace clm {
 
 namespace {
-constexpr int BM = 128, BN = 128, BK = 64;
-constexpr int STAGE_BYTES = (BM + BN) * BK * 2;  // 32 KiB
+constexpr int BK = 64;
 
-template <bool BF, int EPI>
-__global__ __launch_bounds__(256, 2) void gemm_nt_kernel(GemmArgs g) {
-  __shared__ __attribute__((aligned(16))) uint8_t smem[2 * STAGE_BYTES];
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+template <int BM, int BN, int WM, int WN, int STAGES>
+struct Cfg {
+  static constexpr int NW = WM * WN;
+  static constexpr int NT = NW * 64;
+  static constexpr int TM = BM / WM / 16;  // 16-row blocks per wave
+  static constexpr int TN = BN / WN / 16;  // 16-col blocks per wave
+  static constexpr int STAGE_BYTES = (BM + BN) * BK * 2;
+  static constexpr int LDS = STAGES * STAGE_BYTES;
+  static constexpr int LA = BM / 8 / NW;   // A DMA pieces (8 rows) per wave per K-tile
+  static constexpr int LB = BN / 8 / NW;
+  static constexpr int L = LA + LB;        // vmcnt units per K-tile
+  static_assert(BM % (8 * NW) == 0 && BN % (8 * NW) == 0, "rows must split evenly over waves");
+  static_assert(TM >= 1 && TN >= 1, "wave tile too small");
+};
+
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  else if constexpr (N == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+  else if constexpr (N == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  else if constexpr (N == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+  else if constexpr (N == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  else if constexpr (N == 12) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+  else if constexpr (N == 16) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+  else static_assert(N < 0, "unsupported vmcnt");
+}
+
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
+template <bool BF, int EPI, int BM, int BN, int WM, int WN, int STAGES>
+__global__ __launch_bounds__(WM * WN * 64) void gemm_kernel(GemmArgs g) {
+  using C = Cfg<BM, BN, WM, WN, STAGES>;
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int ntn = (g.N + BN - 1) / BN, ntm = (g.M + BM - 1) / BM;
   const int t = xcd_remap(blockIdx.x, ntn * ntm);
   const int tm = t / ntn, tn = t % ntn;
   const int m0 = tm * BM, n0 = tn * BN;
 
-  // each wave stages 32 rows of A and 32 rows of W per K-tile (4 x 1 KiB DMA each)
+  // per-lane DMA sources: piece i of this wave covers tile rows (wid*LA + i)*8 .. +8
   const int r8 = lane >> 3, pc = lane & 7;
-  const u16* a_src[4];
-  const u16* w_src[4];
+  const u16* a_src[C::LA];
+  const u16* w_src[C::LB];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int row = wid * 32 + i * 8 + r8;
-    const int c = pc ^ ((row >> 1) & 7);
-    const int gm = min(m0 + row, g.M - 1);
-    const int gn = min(n0 + row, g.N - 1);
-    a_src[i] = g.A + (int64_t)gm * g.lda + c * 8;
-    w_src[i] = g.W + (int64_t)gn * g.ldw + c * 8;
+  for (int i = 0; i < C::LA; ++i) {
+    const int row = (wid * C::LA + i) * 8 + r8;
+    a_src[i] = g.A + (int64_t)min(m0 + row, g.M - 1) * g.lda + (pc ^ ((row >> 1) & 7)) * 8;
+  }
+#pragma unroll
+  for (int i = 0; i < C::LB; ++i) {
+    const int row = (wid * C::LB + i) * 8 + r8;
+    w_src[i] = g.W + (int64_t)min(n0 + row, g.N - 1) * g.ldw + (pc ^ ((row >> 1) & 7)) * 8;
   }
   auto stage = [&](int kt, int s) {
-    uint8_t* base = smem + s * STAGE_BYTES;
+    uint8_t* base = smem + s * C::STAGE_BYTES;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
+    for (int i = 0; i < C::LA; ++i)
       __builtin_amdgcn_global_load_lds((const void*)(a_src[i] + kt * BK),
-                                       (void*)(base + (wid * 32 + i * 8) * 128), 16, 0, 0);
+                                       (void*)(base + (wid * C::LA + i) * 1024), 16, 0, 0);
+#pragma unroll
+    for (int i = 0; i < C::LB; ++i)
       __builtin_amdgcn_global_load_lds((const void*)(w_src[i] + kt * BK),
-                                       (void*)(base + BM * 128 + (wid * 32 + i * 8) * 128), 16, 0, 0);
-    }
+                                       (void*)(base + BM * 128 + (wid * C::LB + i) * 1024), 16, 0, 0);
   };
 
-  const int wm = wid >> 1, wn = wid & 1;
-  f32x4 acc[4][4];
+  const int wm = wid / WN, wn = wid % WN;
+  f32x4 acc[C::TM][C::TN];
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < C::TM; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < C::TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int nk = g.K / BK;
-  stage(0, 0);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
+#pragma unroll
+  for (int s = 0; s < STAGES - 1; ++s)
+    if (s < nk) stage(s, s);
 
   for (int kt = 0; kt < nk; ++kt) {
-    const int s = kt & 1;
-    if (kt + 1 < nk) stage(kt + 1, s ^ 1);
-    const uint8_t* sa = smem + s * STAGE_BYTES;
+    // retire tile kt's DMA (leave the younger tiles in flight), then one barrier makes
+    // it visible to every wave and proves tile kt-1's buffer is no longer being read
+    if (kt + STAGES - 2 < nk) wait_vmcnt<C::L * (STAGES - 2)>();
+    else wait_vmcnt<0>();
+    lds_barrier();
+    if (kt + STAGES - 1 < nk) stage(kt + STAGES - 1, (kt + STAGES - 1) % STAGES);
+    const uint8_t* sa = smem + (kt % STAGES) * C::STAGE_BYTES;
     const uint8_t* sb = sa + BM * 128;
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
       const int c = kk * 4 + (lane >> 4);
-      u32x4 af[4], bfr[4];
+      u32x4 af[C::TM], bw[C::TN];
 #pragma unroll
-      for (int mb = 0; mb < 4; ++mb) {
-        const int row = wm * 64 + mb * 16 + (lane & 15);
+      for (int mb = 0; mb < C::TM; ++mb) {
+        const int row = wm * (BM / WM) + mb * 16 + (lane & 15);
         af[mb] = *(const u32x4*)(sa + row * 128 + swz(row, c) * 16);
       }
 #pragma unroll
-      for (int nb = 0; nb < 4; ++nb) {
-        const int row = wn * 64 + nb * 16 + (lane & 15);
-        bfr[nb] = *(const u32x4*)(sb + row * 128 + swz(row, c) * 16);
+      for (int nb = 0; nb < C::TN; ++nb) {
+        const int row = wn * (BN / WN) + nb * 16 + (lane & 15);
+        bw[nb] = *(const u32x4*)(sb + row * 128 + swz(row, c) * 16);
       }
 #pragma unroll
-      for (int mb = 0; mb < 4; ++mb)
+      for (int mb = 0; mb < C::TM; ++mb)
 #pragma unroll
-        for (int nb = 0; nb < 4; ++nb) acc[mb][nb] = mfma16<BF>(af[mb], bfr[nb], acc[mb][nb]);
+        for (int nb = 0; nb < C::TN; ++nb) acc[mb][nb] = mfma16<BF>(bw[nb], af[mb], acc[mb][nb]);
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
   }
 
-  // ---- epilogue: C layout col = lane&15, row = (lane>>4)*4 + j -------------
+  // ---- epilogue: lane owns C[m, n..n+3], m = ...+(lane&15), n = ...+(lane>>4)*4 ----
+  const bool nvec = (g.N % 4) == 0 && (g.ldo % 4) == 0;
 #pragma unroll
-  for (int mb = 0; mb < 4; ++mb) {
+  for (int mb = 0; mb < C::TM; ++mb) {
+    const int m = m0 + wm * (BM / WM) + mb * 16 + (lane & 15);
+    if (m >= g.M) continue;
+    float rs = 1.f;
+    int64_t prow = m;
+    const float* aux = nullptr;
+    if constexpr (EPI == EPI_SCORE) rs = g.rscale ? g.rscale[m] : 1.f;
+    if constexpr (EPI == EPI_PATCH) {
+      const int b = m / g.group, p = m - b * g.group;
+      prow = (int64_t)b * (g.group + 1) + 1 + p;
+      aux = g.aux + (int64_t)(1 + p) * g.aux_ld;
+    }
 #pragma unroll
-    for (int nb = 0; nb < 4; ++nb) {
-      const int n = n0 + wn * 64 + nb * 16 + (lane & 15);
+    for (int nb = 0; nb < C::TN; ++nb) {
+      const int n = n0 + wn * (BN / WN) + nb * 16 + (lane >> 4) * 4;
       if (n >= g.N) continue;
-      float bias = 0.f;
-      if constexpr (EPI == EPI_STORE || EPI == EPI_GELU || EPI == EPI_RESID)
-        if (g.bias) bias = g.bias[n];
-      float cs = 1.f;
-      if constexpr (EPI == EPI_SCORE) cs = g.cscale ? g.cscale[n] : 1.f;
+      float v[4] = {acc[mb][nb][0], acc[mb][nb][1], acc[mb][nb][2], acc[mb][nb][3]};
+      if (nvec) {
+        if constexpr (EPI == EPI_STORE || EPI == EPI_GELU || EPI == EPI_RESID) {
+          if (g.bias) {
+            const float4 b4 = *(const float4*)(g.bias + n);
+            v[0] += b4.x; v[1] += b4.y; v[2] += b4.z; v[3] += b4.w;
+          }
+        }
+        if constexpr (EPI == EPI_STORE || EPI == EPI_GELU) {
+          if constexpr (EPI == EPI_GELU) {
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int m = m0 + wm * 64 + mb * 16 + (lane >> 4) * 4 + j;
-        if (m >= g.M) continue;
-        const float v = acc[mb][nb][j];
-        if constexpr (EPI == EPI_STORE) {
-          ((u16*)g.out)[(int64_t)m * g.ldo + n] = from_f32<BF>(v + bias);
-        } else if constexpr (EPI == EPI_GELU) {
-          ((u16*)g.out)[(int64_t)m * g.ldo + n] = from_f32<BF>(quick_gelu(v + bias));
+            for (int j = 0; j < 4; ++j) v[j] = quick_gelu(v[j]);
+          }
+          uint2 o;
+          o.x = pack2<BF>(v[0], v[1]);
+          o.y = pack2<BF>(v[2], v[3]);
+          *(uint2*)((u16*)g.out + (int64_t)m * g.ldo + n) = o;
         } else if constexpr (EPI == EPI_RESID) {
-          float* o = (float*)g.out + (int64_t)m * g.ldo + n;
-          *o = *o + (v + bias);
+          float4* o = (float4*)((float*)g.out + (int64_t)m * g.ldo + n);
+          float4 h = *o;
+          h.x += v[0]; h.y += v[1]; h.z += v[2]; h.w += v[3];
+          *o = h;
         } else if constexpr (EPI == EPI_PATCH) {
-          const int b = m / g.group, p = m - b * g.group;
-          const int64_t row = (int64_t)b * (g.group + 1) + 1 + p;
-          ((float*)g.out)[row * g.ldo + n] = v + g.aux[(int64_t)(1 + p) * g.aux_ld + n];
+          const float4 p4 = *(const float4*)(aux + n);
+          *(float4*)((float*)g.out + prow * g.ldo + n) = make_float4(v[0] + p4.x, v[1] + p4.y, v[2] + p4.z, v[3] + p4.w);
         } else {  // EPI_SCORE
-          const float rs = g.rscale ? g.rscale[m] : 1.f;
-          ((float*)g.out)[(int64_t)m * g.ldo + n] = v * rs * cs;
+          const float4 c4 = g.cscale ? *(const float4*)(g.cscale + n) : make_float4(1.f, 1.f, 1.f, 1.f);
+          *(float4*)((float*)g.out + (int64_t)m * g.ldo + n) =
+              make_float4(v[0] * rs * c4.x, v[1] * rs * c4.y, v[2] * rs * c4.z, v[3] * rs * c4.w);
+        }
+      } else {  // ragged N (not a multiple of 4): scalar tail
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int nj = n + j;
+          if (nj >= g.N) break;
+          float x = v[j];
+          if constexpr (EPI == EPI_STORE || EPI == EPI_GELU || EPI == EPI_RESID)
+            if (g.bias) x += g.bias[nj];
+          if constexpr (EPI == EPI_STORE) ((u16*)g.out)[(int64_t)m * g.ldo + nj] = from_f32<BF>(x);
+          else if constexpr (EPI == EPI_GELU) ((u16*)g.out)[(int64_t)m * g.ldo + nj] = from_f32<BF>(quick_gelu(x));
+          else if constexpr (EPI == EPI_RESID) ((float*)g.out)[(int64_t)m * g.ldo + nj] += x;
+          else if constexpr (EPI == EPI_PATCH) ((float*)g.out)[prow * g.ldo + nj] = x + aux[nj];
+          else ((float*)g.out)[(int64_t)m * g.ldo + nj] = x * rs * (g.cscale ? g.cscale[nj] : 1.f);
         }
       }
     }
   }
 }
 
-template <bool BF>
-hipError_t launch(int epi, const GemmArgs& g, hipStream_t s) {
+template <bool BF, int EPI, int BM, int BN, int WM, int WN, int STAGES>
+hipError_t launch_cfg(const GemmArgs& g, hipStream_t s) {
+  using C = Cfg<BM, BN, WM, WN, STAGES>;
+  auto kern = gemm_kernel<BF, EPI, BM, BN, WM, WN, STAGES>;
+  static unsigned dev_done = 0;   // >64 KiB dynamic LDS needs the opt-in attribute, once per device
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  if (!(__atomic_load_n(&dev_done, __ATOMIC_ACQUIRE) & (1u << (dev & 31)))) {
+    hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, C::LDS);
+    if (e != hipSuccess) return e;
+    __atomic_fetch_or(&dev_done, 1u << (dev & 31), __ATOMIC_RELEASE);
+  }
   const int nwg = ((g.N + BN - 1) / BN) * ((g.M + BM - 1) / BM);
-  dim3 grid(nwg), block(256);
-  switch (epi) {
-    case EPI_STORE: gemm_nt_kernel<BF, EPI_STORE><<<grid, block, 0, s>>>(g); break;
-    case EPI_GELU: gemm_nt_kernel<BF, EPI_GELU><<<grid, block, 0, s>>>(g); break;
-    case EPI_RESID: gemm_nt_kernel<BF, EPI_RESID><<<grid, block, 0, s>>>(g); break;
-    case EPI_PATCH: gemm_nt_kernel<BF, EPI_PATCH><<<grid, block, 0, s>>>(g); break;
-    case EPI_SCORE: gemm_nt_kernel<BF, EPI_SCORE><<<grid, block, 0, s>>>(g); break;
+  kern<<<dim3(nwg), dim3(C::NT), C::LDS, s>>>(g);
+  return hipGetLastError();
+}
+
+// tile configurations (index = GemmArgs-independent id, also the `config` of clm_gemm)
+template <bool BF, int EPI>
+hipError_t launch_id(int id, const GemmArgs& g, hipStream_t s) {
+  switch (id) {
+    case 0: return launch_cfg<BF, EPI, 128, 128, 2, 2, 2>(g, s);
+    case 1: return launch_cfg<BF, EPI, 128, 128, 2, 2, 3>(g, s);
+    case 2: return launch_cfg<BF, EPI, 256, 128, 4, 2, 3>(g, s);
+    case 3: return launch_cfg<BF, EPI, 128, 256, 2, 4, 3>(g, s);
+    case 4: return launch_cfg<BF, EPI, 256, 256, 4, 2, 2>(g, s);
+    case 5: return launch_cfg<BF, EPI, 64, 128, 1, 2, 3>(g, s);
     default: return hipErrorInvalidValue;
   }
-  return hipGetLastError();
+}
+
+constexpr int NCFG = 6;
+constexpr int CFG_BM[NCFG] = {128, 128, 256, 128, 256, 64};
+constexpr int CFG_BN[NCFG] = {128, 128, 128, 256, 256, 128};
+
+// Heuristic: among the 3-stage configs, minimise (waves of work) x (tile cost),
+// where one "wave" is the number of workgroups the chip runs at once.
+int pick_config(int M, int N) {
+  const int cands[] = {1, 2, 3, 5};
+  int best = 1;
+  double best_cost = 1e30;
+  for (int id : cands) {
+    const int64_t tiles = (int64_t)((M + CFG_BM[id] - 1) / CFG_BM[id]) * ((N + CFG_BN[id] - 1) / CFG_BN[id]);
+    const int resident = 256;   // one workgroup per CU at >= 48 KiB LDS x 3 stages
+    const int64_t rounds = (tiles + resident - 1) / resident;
+    // per-tile time ~ (BM*BN) MACs / efficiency(tile): bigger tiles reuse LDS/L2 better
+    const double eff = (CFG_BM[id] * CFG_BN[id]) / (double)(CFG_BM[id] + CFG_BN[id]);  // intensity
+    const double cost = rounds * (double)CFG_BM[id] * CFG_BN[id] / eff;
+    if (cost < best_cost) { best_cost = cost; best = id; }
+  }
+  return best;
+}
+
+template <bool BF>
+hipError_t dispatch(int epi, int id, const GemmArgs& g, hipStream_t s) {
+  switch (epi) {
+    case EPI_STORE: return launch_id<BF, EPI_STORE>(id, g, s);
+    case EPI_GELU: return launch_id<BF, EPI_GELU>(id, g, s);
+    case EPI_RESID: return launch_id<BF, EPI_RESID>(id, g, s);
+    case EPI_PATCH: return launch_id<BF, EPI_PATCH>(id, g, s);
+    case EPI_SCORE: return launch_id<BF, EPI_SCORE>(id, g, s);
+    default: return hipErrorInvalidValue;
+  }
 }
 }  // namespace
 
-hipError_t gemm(bool bf16, int epi, const GemmArgs& g, hipStream_t s) {
+int gemm_num_configs() { return NCFG; }
+
+hipError_t gemm_cfg(bool bf16, int epi, int config, const GemmArgs& g, hipStream_t s) {
   if (g.M <= 0 || g.N <= 0) return hipSuccess;
   if (g.K <= 0 || (g.K % BK) != 0 || (g.lda % 8) != 0 || (g.ldw % 8) != 0) return hipErrorInvalidValue;
-  return bf16 ? launch<true>(epi, g, s) : launch<false>(epi, g, s);
+  const int id = config >= 0 ? config : pick_config(g.M, g.N);
+  return bf16 ? dispatch<true>(epi, id, g, s) : dispatch<false>(epi, id, g, s);
 }
+
+hipError_t gemm(bool bf16, int epi, const GemmArgs& g, hipStream_t s) { return gemm_cfg(bf16, epi, -1, g, s); }
 
 }  // namespace clm

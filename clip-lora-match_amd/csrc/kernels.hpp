@@ -26,6 +26,9 @@ struct GemmArgs {
 };
 
 hipError_t gemm(bool bf16, int epi, const GemmArgs& g, hipStream_t s);
+// explicit tile configuration (config < 0: heuristic); configs: k_gemm.hip launch_id
+hipError_t gemm_cfg(bool bf16, int epi, int config, const GemmArgs& g, hipStream_t s);
+int gemm_num_configs();
 
 // ----------------------------------------------------------- row ops -------
 // LayerNorm over rows of a fp32 matrix, one wave per row.

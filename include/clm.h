@@ -139,6 +139,18 @@ int clm_topk_merge(int hip_device, const float* scores, const int64_t* idx, int6
 /* rows [n, dim] f32 in place (device or host) */
 int clm_l2_normalize(int hip_device, float* rows, int64_t n, int dim, void* stream);
 
+/* Kernel-level entry points (unit tests and micro-benchmarks of the hot kernels).
+ * clm_gemm: C[M,N] = A[M,K] . W[N,K]^T with dtype CLM_BF16|CLM_F16 operands (device
+ * pointers), K % 64 == 0, epilogue CLM_EPI_*; config < 0 picks the tile heuristically. */
+enum { CLM_EPI_STORE = 0, CLM_EPI_GELU = 1, CLM_EPI_RESID = 2, CLM_EPI_SCORE = 4 };
+int clm_gemm(int hip_device, int dtype, int epilogue, int config, const void* A, int64_t lda,
+             const void* W, int64_t ldw, int M, int N, int K, void* out, int64_t ldo,
+             const float* bias, const float* rscale, const float* cscale, void* stream);
+int clm_gemm_num_configs(void);
+/* attention over qkv [B*T, 3*H*64] (q pre-scaled), out [B*T, ldo] (device pointers) */
+int clm_attention(int hip_device, int dtype, int causal, const void* qkv, void* out, int64_t ldo,
+                  int B, int T, int H, void* stream);
+
 /* Kernel timing by category, measured with hipEvents recorded on the launch
  * stream around every kernel of clm_encode_* while enabled (adds event
  * overhead; keep it off in timed regions). categories: CLM_PROF_* */

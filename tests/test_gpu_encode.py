@@ -65,7 +65,7 @@ def test_b32_lora_golden(dtype):
     gt = m.encode_ids(torch.from_numpy(g["ids"]).cuda()).cpu().numpy()
     _check(gi, gt, g["emb_img"], g["emb_txt"], dtype)
     # LoRA must matter far beyond the tolerance (non-vacuous parity)
-    assert np.max(np.abs(g["emb_txt"] - g["emb_txt_base"])) > 20 * TOL[dtype]["score"]
+    assert np.max(np.abs(g["emb_txt"] - g["emb_txt_base"])) > 10 * TOL[dtype]["score"]
 
 
 def test_b32_unmerged_matches_merged():

@@ -1,0 +1,89 @@
+"""Kernel-level numerics through the C-ABI hooks, against plain PyTorch fp32
+references of the same op (GEMM with every epilogue and tile config; attention
+plain and causal at T = 50, 77, 577)."""
+import numpy as np
+import pytest
+import torch
+
+from clip_lora_match_amd import _capi as C
+
+pytestmark = pytest.mark.gpu
+DT = {"bfloat16": (torch.bfloat16, C.CLM_BF16), "float16": (torch.float16, C.CLM_F16)}
+
+
+def _gemm(dtype, epi, cfg, A, W, out, bias=None, rs=None, cs=None):
+    M, K = A.shape
+    N = W.shape[0]
+    p = lambda t: C.ptr(t) if t is not None else None  # noqa: E731
+    C.check(C.lib().clm_gemm(A.device.index, DT[dtype][1], epi, cfg, C.ptr(A), A.stride(0), C.ptr(W), W.stride(0),
+                             M, N, K, C.ptr(out), out.stride(0), p(bias), p(rs), p(cs),
+                             C.stream_of(A.device)), "clm_gemm")
+
+
+@pytest.mark.parametrize("dtype", ["bfloat16", "float16"])
+@pytest.mark.parametrize("cfg", list(range(6)) + [-1])
+@pytest.mark.parametrize("shape", [(333, 200, 128), (1000, 768, 768), (77, 2304, 512)])
+def test_gemm_epilogues_vs_torch(dtype, cfg, shape):
+    M, N, K = shape
+    td = DT[dtype][0]
+    g = torch.Generator(device="cuda").manual_seed(M + N + K)
+    A = torch.randn((M, K), generator=g, device="cuda").to(td)
+    W = (torch.randn((N, K), generator=g, device="cuda") / K ** 0.5).to(td)
+    bias = torch.randn(N, generator=g, device="cuda")
+    ref = A.float() @ W.float().T + bias
+    out = torch.empty((M, N), dtype=td, device="cuda")
+    _gemm(dtype, C.CLM_EPI_STORE, cfg, A, W, out, bias)
+    tol = 2e-2 if dtype == "bfloat16" else 4e-3
+    assert (out.float() - ref).abs().max() <= tol * ref.abs().max()
+    _gemm(dtype, C.CLM_EPI_GELU, cfg, A, W, out, bias)
+    refg = ref * torch.sigmoid(1.702 * ref)
+    assert (out.float() - refg).abs().max() <= tol * refg.abs().max()
+    h = torch.randn((M, N), generator=g, device="cuda")
+    h0 = h.clone()
+    _gemm(dtype, C.CLM_EPI_RESID, cfg, A, W, h, bias)
+    assert (h - (h0 + ref)).abs().max() <= 1e-3 * ref.abs().max() + 1e-5
+    rs = torch.rand(M, generator=g, device="cuda") + 0.5
+    cs = torch.rand(N, generator=g, device="cuda") + 0.5
+    sc = torch.empty((M, N), dtype=torch.float32, device="cuda")
+    _gemm(dtype, C.CLM_EPI_SCORE, cfg, A, W, sc, None, rs, cs)
+    refs = (A.float() @ W.float().T) * rs[:, None] * cs[None, :]
+    assert (sc - refs).abs().max() <= 1e-4 * refs.abs().max() + 1e-6
+
+
+def test_gemm_asymmetric_identity():
+    """A = I catches a transposed C write (cdna_hip_programming §3 'A=I-check with ASYMMETRIC B')."""
+    n = 128
+    A = torch.eye(n, device="cuda", dtype=torch.float16)
+    W = torch.arange(n * n, device="cuda", dtype=torch.float32).reshape(n, n).remainder(97).half()
+    out = torch.empty((n, n), dtype=torch.float16, device="cuda")
+    for cfg in range(6):
+        _gemm("float16", C.CLM_EPI_STORE, cfg, A, W, out)
+        assert torch.equal(out, W.T.contiguous())
+
+
+def _attn_ref(qkv, B, T, H, causal):
+    d = H * 64
+    x = qkv.float().view(B, T, 3, H, 64)
+    q, k, v = (x[:, :, i].transpose(1, 2) for i in range(3))
+    s = q @ k.transpose(-1, -2)      # q already carries the 64^-1/2 scale
+    if causal:
+        s = s + torch.triu(torch.full((T, T), float("-inf"), device=s.device), 1)
+    return (torch.softmax(s, -1) @ v).transpose(1, 2).reshape(B * T, d)
+
+
+@pytest.mark.parametrize("dtype", ["bfloat16", "float16"])
+@pytest.mark.parametrize("B,T,H,causal", [(3, 50, 12, False), (2, 77, 8, True), (2, 77, 8, False),
+                                          (1, 577, 16, False), (2, 130, 2, True), (1, 1, 2, True)])
+def test_attention_vs_torch(dtype, B, T, H, causal):
+    td = DT[dtype][0]
+    g = torch.Generator(device="cuda").manual_seed(T * H)
+    qkv = torch.randn((B * T, 3 * H * 64), generator=g, device="cuda")
+    qkv[:, : H * 64] *= 0.125 * 3
+    qkv = qkv.to(td)
+    out = torch.full((B * T, H * 64 + 64), 7.0, device="cuda").to(td)
+    C.check(C.lib().clm_attention(0, DT[dtype][1], int(causal), C.ptr(qkv), C.ptr(out), out.stride(0), B, T, H,
+                                  C.stream_of(qkv.device)), "clm_attention")
+    ref = _attn_ref(qkv, B, T, H, causal)
+    err = (out[:, : H * 64].float() - ref).abs().max().item()
+    assert err < (3e-2 if dtype == "bfloat16" else 4e-3), err
+    assert (out[:, H * 64:].float() == 7.0).all()   # columns past d untouched

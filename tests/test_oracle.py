@@ -1,0 +1,76 @@
+"""The CPU oracle against the goldens (transformers CLIPModel + the reference's own
+similarity.py outputs), so the GPU parity tests rest on a pinned checker."""
+import numpy as np
+import pytest
+
+from conftest import GOLDEN, golden, synthetic
+
+import clip_lora_match_amd as clm
+from clip_lora_match_amd import synthetic as syn
+from oracle import clip_ref as R
+from oracle import search_ref as S
+
+
+def test_preprocess_is_clip_image_processor_exactly():
+    transformers = pytest.importorskip("transformers")
+    from transformers import CLIPImageProcessor
+    cfg = clm.get_preset("ViT-B/32")
+    imgs = syn.images_u8(2, cfg.image_size, 3)
+    pv = CLIPImageProcessor()(images=list(imgs), return_tensors="np")["pixel_values"]
+    assert np.array_equal(pv, R.preprocess_u8(imgs, cfg.mean, cfg.std))
+
+
+@pytest.mark.parametrize("name,preset", [("enc_tiny_lora.npz", "tiny"), ("enc_b32_lora.npz", "ViT-B/32"),
+                                         ("enc_l14_lora.npz", "ViT-L/14@336")])
+def test_oracle_matches_transformers_golden(name, preset):
+    g = golden(name)
+    cfg, sd, lora = synthetic(preset, True)
+    assert cfg.lora_r == int(g["r"]) and ",".join(cfg.lora_targets) == str(g["targets"])
+    imgs = syn.images_u8(int(g["n_img"]), cfg.image_size, int(g["img_seed"]))
+    ids = syn.captions(int(g["n_txt"]), int(g["L"]), cfg.bos_token_id, cfg.eos_token_id, int(g["cap_seed"]))
+    assert np.array_equal(ids, g["ids"])
+    fi = R.image_features(sd, cfg, R.preprocess_u8(imgs, cfg.mean, cfg.std), lora)
+    ft = R.text_features(sd, cfg, ids, lora)
+    assert np.max(np.abs(fi - g["emb_img"])) < 2e-6
+    assert np.max(np.abs(ft - g["emb_txt"])) < 2e-6
+    # LoRA is not a no-op in the fixtures (non-zero B)
+    assert np.max(np.abs(g["emb_txt"] - g["emb_txt_base"])) > 1e-2
+    assert np.max(np.abs(g["emb_img"] - g["emb_img_base"])) > 1e-3
+
+
+def test_eos_rules_agree_for_clip_ids():
+    cfg = clm.get_preset("ViT-B/32")
+    ids = syn.captions(32, 77, cfg.bos_token_id, cfg.eos_token_id, 5)
+    assert np.array_equal(R.eos_positions(ids, cfg.eos_token_id), R.eos_positions(ids, 2))
+
+
+@pytest.mark.parametrize("k", [1, 5, 10, 50])
+def test_search_oracle_vs_reference_golden(k):
+    g = golden("search_gauss.npz")
+    rows = syn.gaussian_rows(int(g["n"]), int(g["dim"]), int(g["row_seed"]))
+    qs = syn.gaussian_rows(int(g["nq"]), int(g["dim"]), int(g["q_seed"]))
+    exact = S.cosine_scores(qs, rows)
+    vals, idx = S.topk(exact, k)
+    for q in range(qs.shape[0]):
+        assert S.same_topk_up_to_ties(idx[q], g[f"idx_k{k}"][q], exact[q], 2e-6)
+    assert np.max(np.abs(vals - g[f"vals_k{k}"])) < 1e-6
+    assert np.max(np.abs(exact[0] - g["cos_q0"])) < 1e-6
+
+
+def test_custom_index_known_answers():
+    import torch
+    g = golden("custom_index_top3.npz")
+    obj = torch.load(f"{GOLDEN}/custom_items_index.pt", map_location="cpu", weights_only=True)
+    E = obj["embeddings"].float().numpy()
+    assert E.shape == (6, 512) and len(obj["image_paths"]) == 6 and len(obj["texts"]) == 6
+    vals, idx = S.search(E, E, 3)
+    assert idx.tolist() == g["idx"].tolist() == [[0, 1, 2], [1, 2, 0], [2, 1, 5], [3, 4, 5], [4, 3, 5], [5, 2, 4]]
+    assert abs(vals[2, 1] - 0.828312) < 1e-6 and abs(vals[2, 2] - 0.818218) < 1e-6
+
+
+def test_topk_tie_rule_and_tie_comparator():
+    s = np.array([[0.5, 0.9, 0.9, 0.1, 0.9]])
+    v, i = S.topk(s, 3)
+    assert i.tolist() == [[1, 2, 4]]
+    assert S.same_topk_up_to_ties(np.array([1, 4, 2]), np.array([1, 2, 4]), s[0], 1e-9)
+    assert not S.same_topk_up_to_ties(np.array([1, 0, 2]), np.array([1, 2, 4]), s[0], 1e-9)
