@@ -138,7 +138,65 @@ __global__ __launch_bounds__(256) void lora_down_kernel(u16* X, int64_t ldx, int
 }
 
 // -------------------------------------------------------------- patchify ---
-// One thread per 8 consecutive K entries of one patch row.
+// Fast path (p % 8 == 0): one thread per (patch row, ky, 8-pixel run) reads the run's
+// 8 pixels of all channels once (24 B u8 / 3 x 32 B f32) and writes one 16-B chunk
+// per channel at k = c*p*p + ky*p + kx0 (conv weight flatten order [c][ky][kx]).
+template <bool BF>
+__global__ __launch_bounds__(256) void patchify_fast_kernel(const void* pix, int layout, int B, int S, int p,
+                                                            const float* lut, u16* P, int Kp) {
+  __shared__ float slut[3 * 256];
+  for (int i = threadIdx.x; i < 3 * 256; i += blockDim.x) slut[i] = lut[i];
+  __syncthreads();
+  const int G = S / p, runs = p / 8, pp = p * p;
+  const int64_t total = (int64_t)B * G * G * p * runs;
+  for (int64_t w = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; w < total;
+       w += (int64_t)gridDim.x * blockDim.x) {
+    const int run = (int)(w % runs);
+    int64_t q = w / runs;
+    const int ky = (int)(q % p);
+    const int64_t r = q / p;                 // patch row = b*G*G + py*G + px
+    const int b = (int)(r / (G * G));
+    const int pi = (int)(r - (int64_t)b * G * G);
+    const int py = pi / G, px = pi - py * G;
+    const int yy = py * p + ky, xx = px * p + run * 8;
+    float v[3][8];
+    if (layout == 0) {
+      const uint8_t* src = (const uint8_t*)pix + (((int64_t)b * S + yy) * S + xx) * 3;
+      const uint2 w0 = *(const uint2*)src, w1 = *(const uint2*)(src + 8), w2 = *(const uint2*)(src + 16);
+      const uint32_t d[6] = {w0.x, w0.y, w1.x, w1.y, w2.x, w2.y};
+#pragma unroll
+      for (int e = 0; e < 24; ++e) {
+        const uint32_t u = (d[e >> 2] >> ((e & 3) * 8)) & 0xffu;
+        v[e % 3][e / 3] = slut[(e % 3) * 256 + u];
+      }
+    } else {
+#pragma unroll
+      for (int c = 0; c < 3; ++c) {
+        const float* src = (const float*)pix + (((int64_t)b * 3 + c) * S + yy) * S + xx;
+        const float4 a0 = *(const float4*)src, a1 = *(const float4*)(src + 4);
+        v[c][0] = a0.x; v[c][1] = a0.y; v[c][2] = a0.z; v[c][3] = a0.w;
+        v[c][4] = a1.x; v[c][5] = a1.y; v[c][6] = a1.z; v[c][7] = a1.w;
+      }
+    }
+    u16* dst = P + r * Kp + ky * p + run * 8;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      uint4 o;
+      o.x = pack2<BF>(v[c][0], v[c][1]); o.y = pack2<BF>(v[c][2], v[c][3]);
+      o.z = pack2<BF>(v[c][4], v[c][5]); o.w = pack2<BF>(v[c][6], v[c][7]);
+      *(uint4*)(dst + c * pp) = o;
+    }
+  }
+}
+
+// zero the K padding columns [C*p*p, Kp) (only when Kp > C*p*p)
+__global__ void pad_cols_kernel(u16* P, int64_t rows, int k0, int Kp) {
+  const int w = Kp - k0;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < rows * w; i += (int64_t)gridDim.x * blockDim.x)
+    P[(i / w) * Kp + k0 + (i % w)] = 0;
+}
+
+// Generic path (any p, any C): one thread per 8 consecutive K entries of one patch row.
 template <bool BF>
 __global__ __launch_bounds__(256) void patchify_kernel(const void* pix, int layout, int B, int S, int p,
                                                        int C, const float* lut, u16* P, int Kp) {
@@ -195,61 +253,98 @@ __device__ __forceinline__ float block_sum256(float v, float* red) {
   return red[0] + red[1] + red[2] + red[3];
 }
 
-__global__ __launch_bounds__(256) void pool_project_kernel(const float* h, int64_t ldh, int T, int d,
+// One block = RB pooled rows: each wave LayerNorms RB/4 rows into LDS (stored
+// [i][row] so one ds_read_b128 gives 4 rows of element i), then each thread
+// projects its <=4 output columns for all RB rows with coalesced reads of
+// projT [d][D] (read once per block, not once per row), and the block reduces
+// the squared norms for the L2 normalisation.
+constexpr int PRB = 8;
+__global__ __launch_bounds__(256) void pool_project_kernel(const float* h, int64_t ldh, int B, int T, int d,
                                                            const int32_t* ids, int eos, const float* g,
-                                                           const float* bt, float eps, const float* projT,
-                                                           int D, void* out, int out_dtype, int normalize) {
+                                                           const float* bt, float eps, const float* projT, int D,
+                                                           void* out, int out_dtype, int normalize) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
-  float* y = sm;            // d
-  float* red = sm + d;      // 8
-  __shared__ int pos_s;
-  __shared__ int maxv_s;
-  const int b = blockIdx.x, tid = threadIdx.x;
-  int prow = 0;
-  if (ids) {
-    const int32_t* id = ids + (int64_t)b * T;
-    if (tid == 0) { pos_s = INT_MAX; maxv_s = INT_MIN; }
-    __syncthreads();
-    if (eos == 2) {  // legacy rule: argmax(ids), first occurrence
-      for (int t = tid; t < T; t += 256) atomicMax(&maxv_s, id[t]);
-      __syncthreads();
-      for (int t = tid; t < T; t += 256) if (id[t] == maxv_s) atomicMin(&pos_s, t);
-    } else {         // first index of eos; (ids==eos).argmax() is 0 when absent
-      for (int t = tid; t < T; t += 256) if (id[t] == eos) atomicMin(&pos_s, t);
+  float* y = sm;                 // [d][PRB]
+  float* red = sm + d * PRB;     // [4 waves][PRB]
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int b0 = blockIdx.x * PRB;
+  for (int rr = wid; rr < PRB; rr += 4) {
+    const int b = b0 + rr;
+    if (b >= B) {
+      for (int e = lane; e < d; e += 64) y[e * PRB + rr] = 0.f;
+      continue;
     }
-    __syncthreads();
-    prow = pos_s == INT_MAX ? 0 : pos_s;
+    int prow = 0;
+    if (ids) {  // first EOS (or argmax(ids) for the legacy eos_token_id == 2 rule)
+      const int32_t* id = ids + (int64_t)b * T;
+      int best = INT_MAX, bestv = INT_MIN;
+      for (int t = lane; t < T; t += 64) {
+        const int v = id[t];
+        if (eos == 2) { if (v > bestv) { bestv = v; best = t; } }
+        else if (v == eos && t < best) best = t;
+      }
+      if (eos == 2) {
+        for (int o = 32; o > 0; o >>= 1) {
+          const int ov = __shfl_xor(bestv, o, 64), ob = __shfl_xor(best, o, 64);
+          if (ov > bestv || (ov == bestv && ob < best)) { bestv = ov; best = ob; }
+        }
+      } else {
+        for (int o = 32; o > 0; o >>= 1) best = min(best, __shfl_xor(best, o, 64));
+      }
+      prow = best == INT_MAX ? 0 : best;   // (ids == eos).argmax() is 0 when absent
+    }
+    const float* x = h + ((int64_t)b * T + prow) * ldh;
+    float s = 0.f;
+    for (int e = lane; e < d; e += 64) s += x[e];
+    const float mean = wave_sum(s) / d;
+    float v = 0.f;
+    for (int e = lane; e < d; e += 64) { const float t = x[e] - mean; v += t * t; }
+    const float rstd = 1.0f / sqrtf(wave_sum(v) / d + eps);
+    for (int e = lane; e < d; e += 64) y[e * PRB + rr] = (x[e] - mean) * rstd * g[e] + bt[e];
   }
-  const float* x = h + ((int64_t)b * T + prow) * ldh;
-  float s = 0.f;
-  for (int e = tid; e < d; e += 256) { const float v = x[e]; y[e] = v; s += v; }
-  const float mean = block_sum256(s, red) / d;
-  float v = 0.f;
-  for (int e = tid; e < d; e += 256) { const float t = y[e] - mean; v += t * t; }
-  const float rstd = 1.0f / sqrtf(block_sum256(v, red) / d + eps);
-  for (int e = tid; e < d; e += 256) y[e] = (y[e] - mean) * rstd * g[e] + bt[e];
   __syncthreads();
-  float o[4] = {0.f, 0.f, 0.f, 0.f};
+  float acc[PRB][4];
+#pragma unroll
+  for (int r = 0; r < PRB; ++r)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) acc[r][q] = 0.f;
   for (int i = 0; i < d; ++i) {
-    const float yi = y[i];
+    const float4 ya = *(const float4*)(y + i * PRB), yb = *(const float4*)(y + i * PRB + 4);
+    const float yv[PRB] = {ya.x, ya.y, ya.z, ya.w, yb.x, yb.y, yb.z, yb.w};
     const float* pr = projT + (int64_t)i * D;
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const int j = tid + q * 256;
-      if (j < D) o[q] += yi * pr[j];
+      const float w = j < D ? pr[j] : 0.f;
+#pragma unroll
+      for (int r = 0; r < PRB; ++r) acc[r][q] += yv[r] * w;
     }
   }
-  float ss = 0.f;
+  float ss[PRB];
 #pragma unroll
-  for (int q = 0; q < 4; ++q) if (tid + q * 256 < D) ss += o[q] * o[q];
-  const float nrm = normalize ? sqrtf(block_sum256(ss, red)) : 1.0f;
+  for (int r = 0; r < PRB; ++r) {
+    float t = 0.f;
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const int j = tid + q * 256;
-    if (j >= D) continue;
-    const float r = normalize ? o[q] / nrm : o[q];
-    if (out_dtype == 0) ((float*)out)[(int64_t)b * D + j] = r;
-    else ((u16*)out)[(int64_t)b * D + j] = f32_to_f16(r);
+    for (int q = 0; q < 4; ++q) t += acc[r][q] * acc[r][q];
+    ss[r] = wave_sum(t);
+  }
+  if (lane == 0)
+#pragma unroll
+    for (int r = 0; r < PRB; ++r) red[wid * PRB + r] = ss[r];
+  __syncthreads();
+#pragma unroll
+  for (int r = 0; r < PRB; ++r) {
+    const int b = b0 + r;
+    if (b >= B) continue;
+    const float nrm = normalize ? sqrtf(red[r] + red[PRB + r] + red[2 * PRB + r] + red[3 * PRB + r]) : 1.0f;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int j = tid + q * 256;
+      if (j >= D) continue;
+      const float o = normalize ? acc[r][q] / nrm : acc[r][q];
+      if (out_dtype == 0) ((float*)out)[(int64_t)b * D + j] = o;
+      else ((u16*)out)[(int64_t)b * D + j] = f32_to_f16(o);
+    }
   }
 }
 
@@ -312,7 +407,20 @@ hipError_t patchify(bool bf16, const void* pix, int layout, int B, int S, int p,
                     u16* P, int Kp, hipStream_t s) {
   if (B <= 0) return hipSuccess;
   if (Kp % 8) return hipErrorInvalidValue;
-  const int64_t total = (int64_t)B * (S / p) * (S / p) * (Kp / 8);
+  const int G = S / p;
+  if (C == 3 && p % 8 == 0 && (S * 3) % 8 == 0) {
+    const int64_t total = (int64_t)B * G * G * p * (p / 8);
+    const int blocks = (int)std::min<int64_t>((total + 255) / 256, 256 * 32);
+    if (bf16) patchify_fast_kernel<true><<<blocks, 256, 0, s>>>(pix, layout, B, S, p, lut, P, Kp);
+    else patchify_fast_kernel<false><<<blocks, 256, 0, s>>>(pix, layout, B, S, p, lut, P, Kp);
+    if (Kp > 3 * p * p) {
+      const int64_t rows = (int64_t)B * G * G;
+      pad_cols_kernel<<<(int)std::min<int64_t>((rows * (Kp - 3 * p * p) + 255) / 256, 4096), 256, 0, s>>>(
+          P, rows, 3 * p * p, Kp);
+    }
+    return hipGetLastError();
+  }
+  const int64_t total = (int64_t)B * G * G * (Kp / 8);
   const int blocks = (int)std::min<int64_t>((total + 255) / 256, 256 * 16);
   if (bf16) patchify_kernel<true><<<blocks, 256, 0, s>>>(pix, layout, B, S, p, C, lut, P, Kp);
   else patchify_kernel<false><<<blocks, 256, 0, s>>>(pix, layout, B, S, p, C, lut, P, Kp);
@@ -331,9 +439,9 @@ hipError_t pool_project(const float* h, int64_t ldh, int B, int T, int d, const 
                         int out_dtype, int normalize, hipStream_t s) {
   if (B <= 0) return hipSuccess;
   if (D > 1024) return hipErrorInvalidValue;
-  const size_t sm = (size_t)(d + 8) * sizeof(float);
-  pool_project_kernel<<<B, 256, sm, s>>>(h, ldh, T, d, ids, eos, g, bta, eps, projT, D, out, out_dtype,
-                                         normalize);
+  const size_t sm = (size_t)(d * PRB + 4 * PRB) * sizeof(float);
+  pool_project_kernel<<<(B + PRB - 1) / PRB, 256, sm, s>>>(h, ldh, B, T, d, ids, eos, g, bta, eps, projT, D, out,
+                                                           out_dtype, normalize);
   return hipGetLastError();
 }
 

@@ -21,7 +21,7 @@ for st in $STAGES; do
       rc=$?; echo "sweep rc=$rc"; cat gpurun_out/sweep.jsonl | head -80; tail -3 gpurun_out/sweep.err; [ $rc -eq 0 ] || exit $rc ;;
     prof)
       export TMPDIR=/tmp
-      timeout -k 10 900 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run -- python bench.py --no-cpu-baseline ${PROF_ARGS:-} > gpurun_out/prof.log 2>&1
+      timeout -k 10 900 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python bench.py --no-cpu-baseline ${PROF_ARGS:-} > gpurun_out/prof.log 2>&1
       rc=$?; echo "prof rc=$rc"; tail -3 gpurun_out/prof.log
       find gpurun_out/prof -name "*stats*" | head; [ $rc -eq 0 ] || exit $rc ;;
   esac
