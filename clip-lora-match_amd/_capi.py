@@ -18,6 +18,7 @@ CLM_OK, CLM_E_ARG, CLM_E_OOM, CLM_E_HIP, CLM_E_STATE, CLM_E_MISSING = 0, -1, -2,
 CLM_F32, CLM_F16, CLM_BF16, CLM_U8, CLM_I32, CLM_I64 = 0, 1, 2, 3, 4, 5
 CLM_PIX_U8_HWC, CLM_PIX_F32_CHW = 0, 1
 CLM_LORA_MERGED, CLM_LORA_UNMERGED = 0, 1
+CLM_PAIR_GRAPH = 1
 
 
 class TowerDesc(ctypes.Structure):
@@ -65,6 +66,8 @@ def lib():
         "clm_set_lora_enabled": (c_int, [c_void_p, c_int]),
         "clm_encode_image": (c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p, c_int, c_int, c_void_p]),
         "clm_encode_text": (c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p, c_int, c_int, c_void_p]),
+        "clm_encode_pair": (c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p, c_int, c_int, c_void_p, c_void_p,
+                                    c_int, c_int, c_int, c_void_p]),
         "clm_index_create": (c_int, [c_int, c_int64, c_int, POINTER(c_void_p)]),
         "clm_index_destroy": (c_int, [c_void_p]),
         "clm_index_append": (c_int, [c_void_p, c_void_p, c_int, c_int64, c_void_p]),
@@ -98,7 +101,7 @@ def lib():
 
 EXPORTED = (
     "clm_ctx_create", "clm_ctx_destroy", "clm_load_tensor", "clm_finalize", "clm_set_lora_enabled",
-    "clm_encode_image", "clm_encode_text", "clm_index_create", "clm_index_destroy", "clm_index_append",
+    "clm_encode_image", "clm_encode_text", "clm_encode_pair", "clm_index_create", "clm_index_destroy", "clm_index_append",
     "clm_index_size", "clm_index_reset", "clm_index_set_offset", "clm_index_read", "clm_index_search",
     "clm_cosine_scores", "clm_topk_merge", "clm_l2_normalize", "clm_last_error", "clm_version",
     "clm_model_desc_size", "clm_prof_enable", "clm_prof_read", "clm_gemm", "clm_gemm_num_configs",

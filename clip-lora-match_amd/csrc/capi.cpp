@@ -15,6 +15,8 @@
 
 #include <algorithm>
 #include <cmath>
+#include <map>
+#include <tuple>
 #include <cstring>
 #include <string>
 #include <unordered_map>
@@ -118,6 +120,7 @@ struct Tower {
   int64_t maxM = 0;
   float* h = nullptr;
   u16 *X = nullptr, *QKV = nullptr, *O = nullptr, *Hm = nullptr, *P = nullptr;
+  float* pooled = nullptr;  // [max_batch, proj_dim] un-normalised projections
   int64_t ldx = 0, ldo = 0, ldm = 0;
 };
 
@@ -137,6 +140,11 @@ struct clm_ctx {
   void* stage_in = nullptr; size_t stage_in_bytes = 0;
   void* stage_out = nullptr; size_t stage_out_bytes = 0;
   int32_t* ids_dev = nullptr;
+  // two-tower concurrency + graph replay (clm_encode_pair)
+  hipStream_t s_img = nullptr, s_txt = nullptr;
+  hipEvent_t ev_fork = nullptr, ev_txt = nullptr, ev_done = nullptr;
+  typedef std::tuple<const void*, int, int, const void*, int, int, void*, void*, int, int> PairKey;
+  std::map<PairKey, hipGraphExec_t> graphs;
   // kernel timing (clm_prof_*): events recorded on the launch stream
   bool prof = false;
   std::vector<hipEvent_t> ev_pool;
@@ -158,7 +166,12 @@ struct clm_ctx {
     *p = (T*)q;
     return CLM_OK;
   }
+  void drop_graphs() {
+    for (auto& kv : graphs) (void)hipGraphExecDestroy(kv.second);
+    graphs.clear();
+  }
   void free_all() {
+    drop_graphs();
     for (void* p : allocs) (void)hipFree(p);
     allocs.clear();
     if (stage_in) (void)hipFree(stage_in);
@@ -401,6 +414,7 @@ int build_tower(clm_ctx* c, Tower& T, bool vision) {
   if ((r = c->dalloc(&T.QKV, (size_t)T.maxM * 3 * T.d))) return r;
   if ((r = c->dalloc(&T.O, (size_t)T.maxM * T.ldo))) return r;
   if ((r = c->dalloc(&T.Hm, (size_t)T.maxM * T.ldm))) return r;
+  if ((r = c->dalloc(&T.pooled, (size_t)B * d.proj_dim))) return r;
   return CLM_OK;
 }
 
@@ -516,7 +530,7 @@ int encode_image_chunk(clm_ctx* c, const void* pix, int layout, int B, void* out
   if (r) return r;
   { PROF(CLM_PROF_OTHER, (double)B * (T.d * 4.0 + d.proj_dim * 4.0) + (double)T.d * d.proj_dim * 4.0);
     KCHK(pool_project(T.h, T.d, B, Tn, T.d, nullptr, d.eos_token_id, T.fin_g, T.fin_b, d.ln_eps, T.projT,
-                      d.proj_dim, out, out_dtype == CLM_F32 ? 0 : 1, normalize, st)); }
+                      d.proj_dim, T.pooled, out, out_dtype == CLM_F32 ? 0 : 1, normalize, st)); }
   return CLM_OK;
 }
 
@@ -535,7 +549,7 @@ int encode_text_chunk(clm_ctx* c, const int32_t* ids_dev, int B, int L, void* ou
   if (r) return r;
   { PROF(CLM_PROF_OTHER, (double)B * (T.d * 4.0 + d.proj_dim * 4.0 + L * 4.0) + (double)T.d * d.proj_dim * 4.0);
     KCHK(pool_project(T.h, T.d, B, L, T.d, ids_dev, d.eos_token_id, T.fin_g, T.fin_b, d.ln_eps, T.projT,
-                      d.proj_dim, out, out_dtype == CLM_F32 ? 0 : 1, normalize, st)); }
+                      d.proj_dim, T.pooled, out, out_dtype == CLM_F32 ? 0 : 1, normalize, st)); }
   return CLM_OK;
 }
 
@@ -642,6 +656,10 @@ int clm_ctx_destroy(clm_ctx* ctx) {
   (void)hipDeviceSynchronize();
   ctx->free_all();
   for (hipEvent_t e : ctx->ev_pool) (void)hipEventDestroy(e);
+  for (hipEvent_t e : {ctx->ev_fork, ctx->ev_txt, ctx->ev_done})
+    if (e) (void)hipEventDestroy(e);
+  for (hipStream_t q : {ctx->s_img, ctx->s_txt})
+    if (q) (void)hipStreamDestroy(q);
   delete ctx;
   return CLM_OK;
 }
@@ -777,6 +795,86 @@ int clm_encode_text(clm_ctx* ctx, const int32_t* ids, int n, int L, void* out, i
       HIPCHK(hipStreamSynchronize(st));
     }
   }
+  return CLM_OK;
+}
+
+static int pair_launch(clm_ctx* c, const void* pixels, int layout, int n_img, const int32_t* ids, int n_txt,
+                       int L, void* oi, void* ot, int out_dtype, int normalize) {
+  // fork: both tower streams wait on ev_fork (recorded on the origin stream by the caller)
+  HIPCHK(hipStreamWaitEvent(c->s_img, c->ev_fork, 0));
+  HIPCHK(hipStreamWaitEvent(c->s_txt, c->ev_fork, 0));
+  int r = n_img ? encode_image_chunk(c, pixels, layout, n_img, oi, out_dtype, normalize, c->s_img) : CLM_OK;
+  if (r) return r;
+  r = n_txt ? encode_text_chunk(c, ids, n_txt, L, ot, out_dtype, normalize, c->s_txt) : CLM_OK;
+  if (r) return r;
+  HIPCHK(hipEventRecord(c->ev_txt, c->s_txt));
+  HIPCHK(hipStreamWaitEvent(c->s_img, c->ev_txt, 0));   // join on s_img
+  return CLM_OK;
+}
+
+int clm_encode_pair(clm_ctx* ctx, const void* pixels, int pix_layout, int n_img, const int32_t* ids, int n_txt,
+                    int L, void* out_img, void* out_txt, int out_dtype, int normalize, int flags, void* stream) {
+  if (!ctx) return fail(CLM_E_ARG, "null ctx");
+  if (!ctx->finalized) return fail(CLM_E_STATE, "clm_finalize has not been called");
+  const clm_model_desc& d = ctx->desc;
+  if (n_img < 0 || n_txt < 0 || n_img > d.max_batch || n_txt > d.max_batch)
+    return fail(CLM_E_ARG, "clm_encode_pair: 0 <= n <= max_batch per tower");
+  if (pix_layout != CLM_PIX_U8_HWC && pix_layout != CLM_PIX_F32_CHW) return fail(CLM_E_ARG, "bad pix_layout");
+  if (out_dtype != CLM_F32 && out_dtype != CLM_F16) return fail(CLM_E_ARG, "out_dtype must be f32 or f16");
+  if (n_txt && (L <= 0 || L > d.max_pos)) return fail(CLM_E_ARG, "bad sequence length");
+  if ((n_img && (!is_device_ptr(pixels) || !is_device_ptr(out_img))) ||
+      (n_txt && (!is_device_ptr(ids) || !is_device_ptr(out_txt))))
+    return fail(CLM_E_ARG, "clm_encode_pair needs device buffers");
+  if (n_img == 0 && n_txt == 0) return CLM_OK;
+  DeviceGuard g(ctx->dev);
+  hipStream_t st = (hipStream_t)stream;
+  if (!ctx->s_img) {
+    HIPCHK(hipStreamCreateWithFlags(&ctx->s_img, hipStreamNonBlocking));
+    HIPCHK(hipStreamCreateWithFlags(&ctx->s_txt, hipStreamNonBlocking));
+    HIPCHK(hipEventCreateWithFlags(&ctx->ev_fork, hipEventDisableTiming));
+    HIPCHK(hipEventCreateWithFlags(&ctx->ev_txt, hipEventDisableTiming));
+    HIPCHK(hipEventCreateWithFlags(&ctx->ev_done, hipEventDisableTiming));
+  }
+  const bool use_graph = (flags & CLM_PAIR_GRAPH) && !ctx->prof;
+  HIPCHK(hipEventRecord(ctx->ev_fork, st));
+  if (!use_graph) {
+    int r = pair_launch(ctx, pixels, pix_layout, n_img, ids, n_txt, L, out_img, out_txt, out_dtype, normalize);
+    if (r) return r;
+  } else {
+    clm_ctx::PairKey key(pixels, pix_layout, n_img, ids, n_txt, L, out_img, out_txt, out_dtype, normalize);
+    auto it = ctx->graphs.find(key);
+    if (it == ctx->graphs.end()) {
+      if (ctx->graphs.size() >= 16) ctx->drop_graphs();
+      // capture on s_img; the fork edge is the wait on ev_fork recorded outside the capture,
+      // so capture starts after it: wait first, then capture the pure kernel sequence
+      HIPCHK(hipStreamWaitEvent(ctx->s_img, ctx->ev_fork, 0));
+      HIPCHK(hipStreamBeginCapture(ctx->s_img, hipStreamCaptureModeRelaxed));
+      HIPCHK(hipEventRecord(ctx->ev_done, ctx->s_img));            // in-capture fork point
+      HIPCHK(hipStreamWaitEvent(ctx->s_txt, ctx->ev_done, 0));
+      int r = n_img ? encode_image_chunk(ctx, pixels, pix_layout, n_img, out_img, out_dtype, normalize, ctx->s_img)
+                    : CLM_OK;
+      if (!r && n_txt) r = encode_text_chunk(ctx, ids, n_txt, L, out_txt, out_dtype, normalize, ctx->s_txt);
+      hipError_t e1 = hipEventRecord(ctx->ev_txt, ctx->s_txt);
+      hipError_t e2 = hipStreamWaitEvent(ctx->s_img, ctx->ev_txt, 0);
+      hipGraph_t graph = nullptr;
+      hipError_t e3 = hipStreamEndCapture(ctx->s_img, &graph);
+      if (r) { if (graph) (void)hipGraphDestroy(graph); return r; }
+      if (e1 != hipSuccess || e2 != hipSuccess || e3 != hipSuccess) {
+        if (graph) (void)hipGraphDestroy(graph);
+        return fail(CLM_E_HIP, std::string("graph capture: ") + hipGetErrorString(e3 != hipSuccess ? e3 : (e1 != hipSuccess ? e1 : e2)));
+      }
+      hipGraphExec_t exec = nullptr;
+      hipError_t e4 = hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0);
+      (void)hipGraphDestroy(graph);
+      if (e4 != hipSuccess) return fail(CLM_E_HIP, std::string("graph instantiate: ") + hipGetErrorString(e4));
+      it = ctx->graphs.emplace(key, exec).first;
+    } else {
+      HIPCHK(hipStreamWaitEvent(ctx->s_img, ctx->ev_fork, 0));
+    }
+    HIPCHK(hipGraphLaunch(it->second, ctx->s_img));
+  }
+  HIPCHK(hipEventRecord(ctx->ev_done, ctx->s_img));
+  HIPCHK(hipStreamWaitEvent(st, ctx->ev_done, 0));
   return CLM_OK;
 }
 

@@ -138,12 +138,141 @@ __global__ __launch_bounds__(256) void attn_kernel(const u16* qkv, int64_t ldq, 
     for (int nb = 0; nb < 4; ++nb) op[nb * 16] = from_f32<BF>(o[nb][j] * inv);
   }
 }
+// T <= 128: one workgroup per (head, batch), ceil(T/16) waves x 16 query rows; all
+// key tiles (<= 2 x 64) staged once; V^T rows hold 128 keys (272-B stride).
+constexpr int VS2 = 272;
+template <bool BF, bool CAUSAL>
+__global__ __launch_bounds__(512) void attn_small_kernel(const u16* qkv, int64_t ldq, u16* out, int64_t ldo,
+                                                         int T, int d) {
+  __shared__ __attribute__((aligned(16))) uint8_t smem[2 * 8192 + 64 * VS2 + 8 * 2048];
+  const int h = blockIdx.x, b = blockIdx.y;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int nthr = blockDim.x;
+  uint8_t* sK = smem;                     // [2 tiles][64 keys][128 B] swizzled
+  uint8_t* sV = smem + 2 * 8192;          // [64 dims][128 keys] (+pad)
+  uint8_t* sP = smem + 2 * 8192 + 64 * VS2 + wid * 2048;
+  const u16* base = qkv + (int64_t)b * T * ldq;
+  const int ntiles = (T + 63) / 64;
+  for (int ci = tid; ci < ntiles * 512; ci += nthr) {
+    const int key = ci >> 3, c = ci & 7;
+    u32x4 kv = u32x4{0u, 0u, 0u, 0u}, vv = u32x4{0u, 0u, 0u, 0u};
+    if (key < T) {
+      const u16* rp = base + (int64_t)key * ldq + h * 64 + c * 8;
+      kv = *(const u32x4*)(rp + d);
+      vv = *(const u32x4*)(rp + 2 * d);
+    }
+    const int kt = key >> 6, kr = key & 63;
+    *(u32x4*)(sK + kt * 8192 + kr * 128 + swz(kr, c) * 16) = kv;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      *(u16*)(sV + (c * 8 + 2 * e) * VS2 + key * 2) = (u16)(vv[e] & 0xffff);
+      *(u16*)(sV + (c * 8 + 2 * e + 1) * VS2 + key * 2) = (u16)(vv[e] >> 16);
+    }
+  }
+  const int q0 = wid * 16;
+  u32x4 qa[2];
+  {
+    const int r = min(q0 + (lane & 15), T - 1);
+    const u16* qp = base + (int64_t)r * ldq + h * 64;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) qa[kk] = *(const u32x4*)(qp + kk * 32 + 8 * (lane >> 4));
+  }
+  __syncthreads();
+  f32x4 o[4];
+  float mrow[4], lrow[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) { o[j] = f32x4{0.f, 0.f, 0.f, 0.f}; mrow[j] = -INFINITY; lrow[j] = 0.f; }
+  const int nkt = CAUSAL ? min((q0 + 15) / 64 + 1, ntiles) : ntiles;
+  for (int kt = 0; kt < nkt; ++kt) {
+    const uint8_t* tK = sK + kt * 8192;
+    f32x4 sc[4];
+#pragma unroll
+    for (int nb = 0; nb < 4; ++nb) {
+      sc[nb] = f32x4{0.f, 0.f, 0.f, 0.f};
+      const int krow = nb * 16 + (lane & 15);
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        const int c = kk * 4 + (lane >> 4);
+        sc[nb] = mfma16<BF>(qa[kk], *(const u32x4*)(tK + krow * 128 + swz(krow, c) * 16), sc[nb]);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int qi = q0 + (lane >> 4) * 4 + j;
+      float tmax = -INFINITY;
+#pragma unroll
+      for (int nb = 0; nb < 4; ++nb) {
+        const int kj = kt * 64 + nb * 16 + (lane & 15);
+        const bool ok = kj < T && (!CAUSAL || kj <= qi);
+        const float v = ok ? sc[nb][j] : -INFINITY;
+        sc[nb][j] = v;
+        tmax = fmaxf(tmax, v);
+      }
+      tmax = group16_max(tmax);
+      const float mnew = fmaxf(mrow[j], tmax);
+      const float alpha = (mrow[j] == -INFINITY) ? 0.f : __expf(mrow[j] - mnew);
+      mrow[j] = mnew;
+      float rs = 0.f;
+#pragma unroll
+      for (int nb = 0; nb < 4; ++nb) {
+        const float p = __expf(sc[nb][j] - mnew);
+        sc[nb][j] = p;
+        rs += p;
+      }
+      rs = group16_sum(rs);
+      lrow[j] = lrow[j] * alpha + rs;
+#pragma unroll
+      for (int nb = 0; nb < 4; ++nb) o[nb][j] *= alpha;
+    }
+#pragma unroll
+    for (int nb = 0; nb < 4; ++nb) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int row = (lane >> 4) * 4 + j, key = nb * 16 + (lane & 15);
+        *(u16*)(sP + row * 128 + swz(row, key >> 3) * 16 + (key & 7) * 2) = from_f32<BF>(sc[nb][j]);
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const int row = lane & 15, c = kk * 4 + (lane >> 4);
+      const u32x4 pa = *(const u32x4*)(sP + row * 128 + swz(row, c) * 16);
+#pragma unroll
+      for (int nb = 0; nb < 4; ++nb) {
+        const int dim = nb * 16 + (lane & 15);
+        const u32x4 vb = *(const u32x4*)(sV + dim * VS2 + (kt * 64 + kk * 32 + 8 * (lane >> 4)) * 2);
+        o[nb] = mfma16<BF>(pa, vb, o[nb]);
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // P reads done before next tile's P writes
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int qi = q0 + (lane >> 4) * 4 + j;
+    if (qi >= T) continue;
+    const float inv = 1.0f / lrow[j];
+    u16* op = out + ((int64_t)b * T + qi) * ldo + h * 64 + (lane & 15);
+#pragma unroll
+    for (int nb = 0; nb < 4; ++nb) op[nb * 16] = from_f32<BF>(o[nb][j] * inv);
+  }
+}
 }  // namespace
 
 hipError_t attention(bool bf16, bool causal, const u16* qkv, int64_t ldq, u16* out, int64_t ldo, int B, int T,
                      int H, int d, hipStream_t s) {
   if (B <= 0 || T <= 0) return hipSuccess;
   if (d != H * 64 || (ldq % 8) || (ldo % 8)) return hipErrorInvalidValue;
+  if (T <= 128) {
+    dim3 g2(H, B), b2(64 * ((T + 15) / 16));
+    if (bf16) {
+      if (causal) attn_small_kernel<true, true><<<g2, b2, 0, s>>>(qkv, ldq, out, ldo, T, d);
+      else attn_small_kernel<true, false><<<g2, b2, 0, s>>>(qkv, ldq, out, ldo, T, d);
+    } else {
+      if (causal) attn_small_kernel<false, true><<<g2, b2, 0, s>>>(qkv, ldq, out, ldo, T, d);
+      else attn_small_kernel<false, false><<<g2, b2, 0, s>>>(qkv, ldq, out, ldo, T, d);
+    }
+    return hipGetLastError();
+  }
   dim3 grid((T + 63) / 64, H, B), block(256);
   if (bf16) {
     if (causal) attn_kernel<true, true><<<grid, block, 0, s>>>(qkv, ldq, out, ldo, T, d);

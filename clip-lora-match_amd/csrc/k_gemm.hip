@@ -20,6 +20,8 @@
 //    (8 B bf16 / 16 B fp32) instead of 2-byte scatter;
 //  * workgroup ids are remapped XCD-aware so the N-tiles sharing one A row-panel
 //    (and its L2 lines) run on one XCD.
+#include <cstdlib>
+
 #include "kernels.hpp"
 
 namespace clm {
@@ -237,25 +239,26 @@ hipError_t launch_id(int id, const GemmArgs& g, hipStream_t s) {
 }
 
 constexpr int NCFG = 6;
-constexpr int CFG_BM[NCFG] = {128, 128, 256, 128, 256, 64};
-constexpr int CFG_BN[NCFG] = {128, 128, 128, 256, 256, 128};
 
-// Heuristic: among the 3-stage configs, minimise (waves of work) x (tile cost),
-// where one "wave" is the number of workgroups the chip runs at once.
+// Tile choice (measured, profiles/r01_v2_gemm_sweep.jsonl): the 2-stage 128x128 tile
+// (64 KiB LDS -> 2 workgroups per CU) wins on the encoder's narrow / short-K GEMMs;
+// the 256x256 tile (1 workgroup per CU) wins when its tile count fills the last
+// round of 256 CUs well (qkv: 1.76-1.80 rounds; square 4096^3: 1.0), and loses when
+// a mostly-empty last round remains (fc1: 2.3-2.4 rounds). $CLM_GEMM_CFG overrides.
 int pick_config(int M, int N) {
-  const int cands[] = {1, 2, 3, 5};
-  int best = 1;
-  double best_cost = 1e30;
-  for (int id : cands) {
-    const int64_t tiles = (int64_t)((M + CFG_BM[id] - 1) / CFG_BM[id]) * ((N + CFG_BN[id] - 1) / CFG_BN[id]);
-    const int resident = 256;   // one workgroup per CU at >= 48 KiB LDS x 3 stages
-    const int64_t rounds = (tiles + resident - 1) / resident;
-    // per-tile time ~ (BM*BN) MACs / efficiency(tile): bigger tiles reuse LDS/L2 better
-    const double eff = (CFG_BM[id] * CFG_BN[id]) / (double)(CFG_BM[id] + CFG_BN[id]);  // intensity
-    const double cost = rounds * (double)CFG_BM[id] * CFG_BN[id] / eff;
-    if (cost < best_cost) { best_cost = cost; best = id; }
+  static int forced = -2;
+  if (forced == -2) {
+    const char* e = getenv("CLM_GEMM_CFG");
+    forced = e ? atoi(e) : -1;
   }
-  return best;
+  if (forced >= 0 && forced < NCFG) return forced;
+  const int64_t t256 = (int64_t)((M + 255) / 256) * ((N + 255) / 256);
+  if (N >= 1024 && t256 >= 256) {
+    const double rounds = t256 / 256.0;
+    const double frac = rounds - (int64_t)rounds;
+    if (frac == 0.0 || frac >= 0.7) return 4;
+  }
+  return 0;
 }
 
 template <bool BF>

@@ -244,28 +244,20 @@ __global__ void write_cls_kernel(float* h, int64_t ldh, int B, int T, int d, con
 }
 
 // ------------------------------------------------------- pool + projection --
-__device__ __forceinline__ float block_sum256(float v, float* red) {
-  v = wave_sum(v);
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  __syncthreads();
-  if (lane == 0) red[wid] = v;
-  __syncthreads();
-  return red[0] + red[1] + red[2] + red[3];
-}
 
-// One block = RB pooled rows: each wave LayerNorms RB/4 rows into LDS (stored
-// [i][row] so one ds_read_b128 gives 4 rows of element i), then each thread
-// projects its <=4 output columns for all RB rows with coalesced reads of
-// projT [d][D] (read once per block, not once per row), and the block reduces
-// the squared norms for the L2 normalisation.
+// Grid (B/PRB row blocks) x (D/64 column blocks). Each block LayerNorms its PRB
+// pooled rows into LDS (layout [i][row]: one ds_read_b128 = 4 rows of element i),
+// then thread (c, part) accumulates column c over a quarter of d for all PRB rows
+// with coalesced projT [d][D] reads; the 4 parts are summed through LDS. The
+// un-normalised rows go to `tmp`; finish_rows_kernel applies the L2 norm.
 constexpr int PRB = 8;
 __global__ __launch_bounds__(256) void pool_project_kernel(const float* h, int64_t ldh, int B, int T, int d,
                                                            const int32_t* ids, int eos, const float* g,
                                                            const float* bt, float eps, const float* projT, int D,
-                                                           void* out, int out_dtype, int normalize) {
+                                                           float* tmp) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
-  float* y = sm;                 // [d][PRB]
-  float* red = sm + d * PRB;     // [4 waves][PRB]
+  float* y = sm;                   // [d][PRB]
+  float* part_sum = sm + d * PRB;  // [4][PRB][64]
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int b0 = blockIdx.x * PRB;
   for (int rr = wid; rr < PRB; rr += 4) {
@@ -303,48 +295,49 @@ __global__ __launch_bounds__(256) void pool_project_kernel(const float* h, int64
     for (int e = lane; e < d; e += 64) y[e * PRB + rr] = (x[e] - mean) * rstd * g[e] + bt[e];
   }
   __syncthreads();
-  float acc[PRB][4];
+  const int c = lane, part = wid;
+  const int j = blockIdx.y * 64 + c;
+  const int i0 = part * (d / 4), i1 = i0 + d / 4;
+  float acc[PRB];
 #pragma unroll
-  for (int r = 0; r < PRB; ++r)
-#pragma unroll
-    for (int q = 0; q < 4; ++q) acc[r][q] = 0.f;
-  for (int i = 0; i < d; ++i) {
-    const float4 ya = *(const float4*)(y + i * PRB), yb = *(const float4*)(y + i * PRB + 4);
-    const float yv[PRB] = {ya.x, ya.y, ya.z, ya.w, yb.x, yb.y, yb.z, yb.w};
-    const float* pr = projT + (int64_t)i * D;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int j = tid + q * 256;
-      const float w = j < D ? pr[j] : 0.f;
-#pragma unroll
-      for (int r = 0; r < PRB; ++r) acc[r][q] += yv[r] * w;
+  for (int r = 0; r < PRB; ++r) acc[r] = 0.f;
+  if (j < D) {
+#pragma unroll 8
+    for (int i = i0; i < i1; ++i) {
+      const float w = projT[(int64_t)i * D + j];
+      const float4 ya = *(const float4*)(y + i * PRB), yb = *(const float4*)(y + i * PRB + 4);
+      acc[0] += ya.x * w; acc[1] += ya.y * w; acc[2] += ya.z * w; acc[3] += ya.w * w;
+      acc[4] += yb.x * w; acc[5] += yb.y * w; acc[6] += yb.z * w; acc[7] += yb.w * w;
     }
   }
-  float ss[PRB];
 #pragma unroll
-  for (int r = 0; r < PRB; ++r) {
-    float t = 0.f;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) t += acc[r][q] * acc[r][q];
-    ss[r] = wave_sum(t);
-  }
-  if (lane == 0)
-#pragma unroll
-    for (int r = 0; r < PRB; ++r) red[wid * PRB + r] = ss[r];
+  for (int r = 0; r < PRB; ++r) part_sum[(part * PRB + r) * 64 + c] = acc[r];
   __syncthreads();
+  if (part == 0 && j < D) {
 #pragma unroll
-  for (int r = 0; r < PRB; ++r) {
-    const int b = b0 + r;
-    if (b >= B) continue;
-    const float nrm = normalize ? sqrtf(red[r] + red[PRB + r] + red[2 * PRB + r] + red[3 * PRB + r]) : 1.0f;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int j = tid + q * 256;
-      if (j >= D) continue;
-      const float o = normalize ? acc[r][q] / nrm : acc[r][q];
-      if (out_dtype == 0) ((float*)out)[(int64_t)b * D + j] = o;
-      else ((u16*)out)[(int64_t)b * D + j] = f32_to_f16(o);
+    for (int r = 0; r < PRB; ++r) {
+      const int b = b0 + r;
+      if (b >= B) continue;
+      tmp[(int64_t)b * D + j] = part_sum[r * 64 + c] + part_sum[(PRB + r) * 64 + c] +
+                                part_sum[(2 * PRB + r) * 64 + c] + part_sum[(3 * PRB + r) * 64 + c];
     }
+  }
+}
+
+// out[b] = tmp[b] / ||tmp[b]||_2 (models/clip_model.py:116,148) or a plain copy; f32 or f16 out
+__global__ __launch_bounds__(256) void finish_rows_kernel(const float* tmp, int B, int D, void* out, int out_dtype,
+                                                          int normalize) {
+  const int lane = threadIdx.x & 63;
+  const int b = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (b >= B) return;
+  const float* r = tmp + (int64_t)b * D;
+  float s = 0.f;
+  for (int e = lane; e < D; e += 64) s += r[e] * r[e];
+  const float nrm = normalize ? sqrtf(wave_sum(s)) : 1.f;
+  for (int e = lane; e < D; e += 64) {
+    const float o = normalize ? r[e] / nrm : r[e];
+    if (out_dtype == 0) ((float*)out)[(int64_t)b * D + e] = o;
+    else ((u16*)out)[(int64_t)b * D + e] = f32_to_f16(o);
   }
 }
 
@@ -435,13 +428,14 @@ hipError_t write_cls(float* h, int64_t ldh, int B, int T, int d, const float* cl
 }
 
 hipError_t pool_project(const float* h, int64_t ldh, int B, int T, int d, const int32_t* ids, int eos,
-                        const float* g, const float* bta, float eps, const float* projT, int D, void* out,
+                        const float* g, const float* bta, float eps, const float* projT, int D, float* tmp, void* out,
                         int out_dtype, int normalize, hipStream_t s) {
   if (B <= 0) return hipSuccess;
-  if (D > 1024) return hipErrorInvalidValue;
-  const size_t sm = (size_t)(d * PRB + 4 * PRB) * sizeof(float);
-  pool_project_kernel<<<(B + PRB - 1) / PRB, 256, sm, s>>>(h, ldh, B, T, d, ids, eos, g, bta, eps, projT, D, out,
-                                                           out_dtype, normalize);
+  if (d % 4) return hipErrorInvalidValue;
+  const size_t sm = (size_t)(d * PRB + 4 * PRB * 64) * sizeof(float);
+  dim3 grid((B + PRB - 1) / PRB, (D + 63) / 64);
+  pool_project_kernel<<<grid, 256, sm, s>>>(h, ldh, B, T, d, ids, eos, g, bta, eps, projT, D, tmp);
+  finish_rows_kernel<<<(B + 3) / 4, 256, 0, s>>>(tmp, B, D, out, out_dtype, normalize);
   return hipGetLastError();
 }
 

@@ -66,9 +66,10 @@ hipError_t write_cls(float* h, int64_t ldh, int B, int T, int d, const float* cl
 
 // pooled row -> LN -> projection (fp32, projT [d, D]) -> optional L2 norm -> out
 //   ids == null: row b*T (CLS); else row b*T + (first eos in ids[b]) (argmax if eos==2)
+//   tmp: [B, D] fp32 workspace
 hipError_t pool_project(const float* h, int64_t ldh, int B, int T, int d, const int32_t* ids,
                         int eos, const float* g, const float* bta, float eps, const float* projT,
-                        int D, void* out, int out_dtype, int normalize, hipStream_t s);
+                        int D, float* tmp, void* out, int out_dtype, int normalize, hipStream_t s);
 
 // ----------------------------------------------------------- attention -----
 // qkv [B*T, 3d] (q pre-scaled by head_dim^-0.5), out [B*T, ldo] compute dtype.

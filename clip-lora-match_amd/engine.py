@@ -126,6 +126,32 @@ class ClipLoraModel:
                                         C.stream_of(self.device)), "clm_encode_text")
         return res
 
+    def encode_pair(self, pixels: torch.Tensor, ids: torch.Tensor, normalize: bool = True,
+                    out_dtype=torch.float32, out_img: Optional[torch.Tensor] = None,
+                    out_txt: Optional[torch.Tensor] = None, graph: bool = True):
+        """Image batch + caption batch (device tensors, each <= max_batch) encoded concurrently on
+        two streams; graph=True replays a captured hipGraph for repeated identical calls."""
+        S = self.cfg.image_size
+        if pixels.dtype == torch.uint8 and tuple(pixels.shape[1:]) == (S, S, self.cfg.channels):
+            layout = C.CLM_PIX_U8_HWC
+        elif pixels.dtype == torch.float32 and tuple(pixels.shape[1:]) == (self.cfg.channels, S, S):
+            layout = C.CLM_PIX_F32_CHW
+        else:
+            raise ValueError("pixels must be uint8 NHWC or float32 NCHW of the model's image size")
+        if ids.dim() != 2 or ids.dtype != torch.int32:
+            raise ValueError("ids must be int32 [n, L]")
+        if not (pixels.is_cuda and ids.is_cuda):
+            raise ValueError("encode_pair needs device tensors")
+        pixels, ids = pixels.contiguous(), ids.contiguous()
+        oi = self._out(pixels.shape[0], out_dtype, out_img)
+        ot = self._out(ids.shape[0], out_dtype, out_txt)
+        code = C.CLM_F32 if out_dtype == torch.float32 else C.CLM_F16
+        C.check(C.lib().clm_encode_pair(self._ctx, C.ptr(pixels), layout, pixels.shape[0], C.ptr(ids),
+                                        ids.shape[0], ids.shape[1], C.ptr(oi), C.ptr(ot), code, int(normalize),
+                                        C.CLM_PAIR_GRAPH if graph else 0, C.stream_of(self.device)),
+                "clm_encode_pair")
+        return oi, ot
+
     # ------------------------------------------------------------ timing --
     def prof_enable(self, enable: bool = True) -> None:
         C.check(C.lib().clm_prof_enable(self._ctx, int(bool(enable))), "clm_prof_enable")

@@ -109,6 +109,16 @@ int clm_encode_image(clm_ctx* ctx, const void* pixels, int pix_layout, int n, vo
 int clm_encode_text(clm_ctx* ctx, const int32_t* ids, int n, int L, void* out, int out_dtype,
                     int normalize, void* stream);
 
+/* One image batch and one caption batch (each <= max_batch, device pointers) encoded
+ * concurrently: the towers run on two context-owned streams forked from / joined to
+ * `stream` with events. flags & CLM_PAIR_GRAPH: the whole launch sequence is captured
+ * once per (pointers, shapes) into a hipGraph and replayed on later calls. Results are
+ * identical to clm_encode_image + clm_encode_text. */
+enum { CLM_PAIR_GRAPH = 1 };
+int clm_encode_pair(clm_ctx* ctx, const void* pixels, int pix_layout, int n_img, const int32_t* ids,
+                    int n_txt, int L, void* out_img, void* out_txt, int out_dtype, int normalize,
+                    int flags, void* stream);
+
 /* GPU-resident index of fp16 rows + fp32 inverse norms (score = q . row / ||row||) */
 int clm_index_create(int hip_device, int64_t capacity, int dim, clm_index** out);
 int clm_index_destroy(clm_index* idx);

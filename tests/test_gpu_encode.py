@@ -150,3 +150,25 @@ def test_bad_inputs_raise():
         m.encode_ids(torch.zeros((1, cfg.max_pos + 1), dtype=torch.int32).cuda())
     with pytest.raises(ValueError):   # token id outside the vocabulary (host ids are validated)
         m.encode_ids(torch.full((1, 4), cfg.vocab + 5, dtype=torch.int32))
+
+
+@pytest.mark.parametrize("graph", [False, True])
+def test_encode_pair_matches_separate(graph):
+    """Two-stream (and graph-replayed) pair encode == the single-tower calls, bit for bit;
+    a replayed graph sees new input contents behind the same pointers."""
+    m, cfg, sd, lora = _model("tiny", "float16", max_batch=16)
+    imgs = torch.from_numpy(syn.images_u8(7, cfg.image_size, 31)).cuda()
+    ids = torch.from_numpy(syn.captions(5, cfg.max_pos, cfg.bos_token_id, cfg.eos_token_id, 32)).cuda()
+    a_i = m.encode_pixels(imgs)
+    a_t = m.encode_ids(ids)
+    oi = torch.empty_like(a_i)
+    ot = torch.empty_like(a_t)
+    for _ in range(3):
+        m.encode_pair(imgs, ids, out_img=oi, out_txt=ot, graph=graph)
+        torch.cuda.synchronize()
+        assert torch.equal(oi, a_i) and torch.equal(ot, a_t)
+    imgs.copy_(torch.from_numpy(syn.images_u8(7, cfg.image_size, 41)).cuda())
+    m.encode_pair(imgs, ids, out_img=oi, out_txt=ot, graph=graph)
+    assert torch.equal(oi, m.encode_pixels(imgs))
+    with pytest.raises(ValueError):
+        m.encode_pair(imgs.cpu(), ids)
