@@ -17,6 +17,7 @@
 #include <cmath>
 #include <map>
 #include <tuple>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <unordered_map>
@@ -189,8 +190,12 @@ struct clm_index {
   int64_t cap = 0, n = 0, dim = 0, offset = 0;
   u16* rows = nullptr;
   float* inv = nullptr;
-  // search workspace (grown on demand)
+  // search workspaces (grown on demand): ws = query staging, ws2 = path buffers
   void* ws = nullptr; size_t ws_bytes = 0;
+  void* ws2 = nullptr; size_t ws2_bytes = 0;
+  // strided row sample for the threshold pass, rebuilt when n changes
+  u16* samp = nullptr; float* samp_inv = nullptr; int64_t samp_S = 0, samp_n = -1, samp_cap = 0;
+  int64_t search_stats[3] = {0, 0, 0};   // filtered queries, exact queries, overflow fallbacks
 };
 
 namespace {
@@ -904,6 +909,9 @@ int clm_index_destroy(clm_index* x) {
   if (x->rows) (void)hipFree(x->rows);
   if (x->inv) (void)hipFree(x->inv);
   if (x->ws) (void)hipFree(x->ws);
+  if (x->ws2) (void)hipFree(x->ws2);
+  if (x->samp) (void)hipFree(x->samp);
+  if (x->samp_inv) (void)hipFree(x->samp_inv);
   delete x;
   return CLM_OK;
 }
@@ -991,38 +999,28 @@ int clm_index_read(clm_index* x, int64_t start, int64_t n, float* dst, void* str
   return CLM_OK;
 }
 
-static int ws_ensure(clm_index* x, size_t bytes) {
-  if (x->ws_bytes >= bytes) return CLM_OK;
-  if (x->ws) (void)hipFree(x->ws);
-  x->ws = nullptr;
-  x->ws_bytes = 0;
-  if (hipMalloc(&x->ws, bytes) != hipSuccess) {
+static int grow(void** p, size_t* cap, size_t bytes) {
+  if (*cap >= bytes) return CLM_OK;
+  if (*p) (void)hipFree(*p);
+  *p = nullptr;
+  *cap = 0;
+  if (hipMalloc(p, bytes) != hipSuccess) {
     (void)hipGetLastError();
     return fail(CLM_E_OOM, "search workspace allocation failed");
   }
-  x->ws_bytes = bytes;
+  *cap = bytes;
   return CLM_OK;
 }
 
-// queries -> fp16 rows + fp32 inverse norms of the source values (for a query the scale only
-// changes the score value, never the order)
-int clm_index_search(clm_index* x, const void* q, int q_dtype, int64_t nq, int k, float* out_scores,
-                     int64_t* out_idx, void* stream) {
-  if (!x || nq < 0 || (nq > 0 && (!q || !out_scores || !out_idx))) return fail(CLM_E_ARG, "bad argument");
-  if (q_dtype != CLM_F32 && q_dtype != CLM_F16) return fail(CLM_E_ARG, "queries must be f32 or f16");
-  if (k < 1 || k > 1024) return fail(CLM_E_ARG, "k must be in [1, 1024]");
-  if (nq == 0) return CLM_OK;
-  DeviceGuard g(x->dev);
-  hipStream_t st = (hipStream_t)stream;
+// Exact path: score chunks [nqb, ch] by the EPI_SCORE GEMM, radix top-k per chunk row,
+// merge the chunk lists. Any k <= 1024, any N.
+static int search_exact(clm_index* x, const u16* q16, const float* qinv, int64_t nq, int k, float* osc,
+                        int64_t* oix, hipStream_t st) {
   const int dim = (int)x->dim;
   const int64_t N = x->n;
-  const bool q_dev = is_device_ptr(q);
-  const bool o_dev = is_device_ptr(out_scores) && is_device_ptr(out_idx);
-
-  // chunking: nchunks * k <= 8192 (merge sort size), score buffer <= budget
   const size_t budget = (size_t)512 << 20;
   const int64_t max_chunks = std::max<int64_t>(1, 8192 / k);
-  int64_t ch = std::max<int64_t>(1, N);
+  int64_t ch = 1;
   if (N > 0) {
     ch = std::max<int64_t>((N + max_chunks - 1) / max_chunks, std::min<int64_t>(N, 1 << 17));
     ch = round_up(ch, 128);
@@ -1030,36 +1028,17 @@ int clm_index_search(clm_index* x, const void* q, int q_dtype, int64_t nq, int k
   const int64_t nchunks = N > 0 ? (N + ch - 1) / ch : 0;
   int64_t nqb = std::max<int64_t>(1, std::min<int64_t>(nq, (int64_t)(budget / ((size_t)ch * 4))));
   nqb = std::min<int64_t>(nqb, 4096);
-
-  // workspace layout: q16 [nq, dim] | qinv [nq] | scores [nqb, ch] | cand_s/cand_i [nqb, nchunks*k] | out staging
-  const size_t q_src_bytes = (size_t)nq * dim * (q_dtype == CLM_F32 ? 4 : 2);
   size_t off = 0;
   auto take = [&](size_t bytes) { size_t o = off; off = round_up(off + bytes, 256); return o; };
-  const size_t o_qsrc = q_dev ? 0 : take(q_src_bytes);
-  const size_t o_q16 = take((size_t)nq * dim * 2);
-  const size_t o_qinv = take((size_t)nq * 4);
-  const size_t o_sc = take((size_t)nqb * std::max<int64_t>(ch, 1) * 4);
+  const size_t o_sc = take((size_t)nqb * ch * 4);
   const size_t o_cs = take((size_t)nqb * std::max<int64_t>(nchunks, 1) * k * 4);
   const size_t o_ci = take((size_t)nqb * std::max<int64_t>(nchunks, 1) * k * 8);
-  const size_t o_os = o_dev ? 0 : take((size_t)nq * k * 4);
-  const size_t o_oi = o_dev ? 0 : take((size_t)nq * k * 8);
-  int r = ws_ensure(x, off);
+  int r = grow(&x->ws2, &x->ws2_bytes, off);
   if (r) return r;
-  uint8_t* ws = (uint8_t*)x->ws;
-  const void* qsrc = q;
-  if (!q_dev) {
-    HIPCHK(hipMemcpyAsync(ws + o_qsrc, q, q_src_bytes, hipMemcpyHostToDevice, st));
-    qsrc = ws + o_qsrc;
-  }
-  u16* q16 = (u16*)(ws + o_q16);
-  float* qinv = (float*)(ws + o_qinv);
-  // inverse norms of the SOURCE rows (reference normalises the fp32 query, search.py:93)
-  KCHK(rows_to_f16(qsrc, q_dtype == CLM_F32 ? 0 : 1, nq, dim, q16, qinv, st, 1));
-  float* osc = o_dev ? out_scores : (float*)(ws + o_os);
-  int64_t* oix = o_dev ? out_idx : (int64_t*)(ws + o_oi);
-  float* sc = (float*)(ws + o_sc);
-  float* cs = (float*)(ws + o_cs);
-  int64_t* ci = (int64_t*)(ws + o_ci);
+  uint8_t* w = (uint8_t*)x->ws2;
+  float* sc = (float*)(w + o_sc);
+  float* cs = (float*)(w + o_cs);
+  int64_t* ci = (int64_t*)(w + o_ci);
   for (int64_t q0 = 0; q0 < nq; q0 += nqb) {
     const int64_t nb = std::min(nqb, nq - q0);
     if (N == 0) {
@@ -1081,6 +1060,139 @@ int clm_index_search(clm_index* x, const void* q, int q_dtype, int64_t nq, int k
     }
     if (nchunks > 1) KCHK(topk_merge(cs, ci, nb, (int)nchunks, k, k, osc + q0 * k, oix + q0 * k, st));
   }
+  return CLM_OK;
+}
+
+// Filtered path (large N, k <= 256), one pass over the index:
+//  1. theta[q] = k-th best score of q over a strided sample of S rows (exact path on the
+//     sample). The sample is a subset of the index, so theta[q] <= the true k-th best.
+//  2. the EPI_FILTER GEMM streams the whole index once (M-fastest tile order: each index
+//     tile is read once and shared by all query tiles) and appends every (score, row) with
+//     score >= theta[q] to q's candidate list (expected ~k*N/S = 256 entries, capacity CAP).
+//     Scores are bit-identical to the sample pass (same K order per dot product), so the
+//     candidates contain the exact top-k, ties included.
+//  3. per-query sort of the candidates (topk_merge) -> (score desc, index asc).
+//  Queries whose list overflowed CAP are redone on the exact path.
+constexpr int CAND_CAP = 2048;
+static int search_filtered(clm_index* x, const u16* q16, const float* qinv, int64_t nq, int k, int64_t S,
+                           float* osc, int64_t* oix, hipStream_t st) {
+  const int dim = (int)x->dim;
+  const int64_t N = x->n;
+  int r;
+  if (x->samp_n != N || x->samp_S != S) {
+    if (x->samp_cap < S) {
+      if (x->samp) (void)hipFree(x->samp);
+      if (x->samp_inv) (void)hipFree(x->samp_inv);
+      x->samp = nullptr; x->samp_inv = nullptr; x->samp_cap = 0;
+      if (hipMalloc(&x->samp, (size_t)S * dim * 2) != hipSuccess || hipMalloc(&x->samp_inv, (size_t)S * 4) != hipSuccess) {
+        (void)hipGetLastError();
+        return fail(CLM_E_OOM, "sample allocation failed");
+      }
+      x->samp_cap = S;
+    }
+    KCHK(sample_rows(x->rows, x->inv, N, dim, S, x->samp, x->samp_inv, st));
+    x->samp_n = N;
+    x->samp_S = S;
+  }
+  const int64_t nqb = std::min<int64_t>(nq, std::max<int64_t>(256, ((int64_t)256 << 20) / ((int64_t)S * 4)));
+  size_t off = 0;
+  auto take = [&](size_t bytes) { size_t o = off; off = round_up(off + bytes, 256); return o; };
+  const size_t o_sc = take((size_t)nqb * S * 4);
+  const size_t o_ts = take((size_t)nqb * k * 4);
+  const size_t o_ti = take((size_t)nqb * k * 8);
+  const size_t o_cnt = take((size_t)nqb * 4);
+  const size_t o_cs = take((size_t)nqb * CAND_CAP * 4);
+  const size_t o_ci = take((size_t)nqb * CAND_CAP * 8);
+  if ((r = grow(&x->ws2, &x->ws2_bytes, off))) return r;
+  uint8_t* w = (uint8_t*)x->ws2;
+  float* sc = (float*)(w + o_sc);
+  float* ts = (float*)(w + o_ts);
+  int64_t* ti = (int64_t*)(w + o_ti);
+  int* cnt = (int*)(w + o_cnt);
+  float* cs = (float*)(w + o_cs);
+  int64_t* ci = (int64_t*)(w + o_ci);
+  std::vector<int> hcnt;
+  std::vector<int64_t> overflow;
+  for (int64_t q0 = 0; q0 < nq; q0 += nqb) {
+    const int64_t nb = std::min(nqb, nq - q0);
+    GemmArgs ga{};
+    ga.A = q16 + q0 * dim; ga.lda = dim; ga.W = x->samp; ga.ldw = dim;
+    ga.M = (int)nb; ga.N = (int)S; ga.K = dim; ga.out = sc; ga.ldo = S;
+    ga.rscale = qinv + q0; ga.cscale = x->samp_inv;
+    KCHK(gemm(false, EPI_SCORE, ga, st));
+    KCHK(topk_rows(sc, S, nb, S, k, 0, ts, ti, k, st));
+    HIPCHK(hipMemsetAsync(cnt, 0, (size_t)nb * 4, st));
+    HIPCHK(hipMemsetAsync(ci, 0xFF, (size_t)nb * CAND_CAP * 8, st));
+    GemmArgs gf{};
+    gf.A = q16 + q0 * dim; gf.lda = dim; gf.W = x->rows; gf.ldw = dim;
+    gf.M = (int)nb; gf.N = (int)N; gf.K = dim;
+    gf.rscale = qinv + q0; gf.cscale = x->inv;
+    gf.theta = ts + (k - 1); gf.theta_ld = k;
+    gf.cnt = cnt; gf.cand_s = cs; gf.cand_i = ci; gf.cap = CAND_CAP; gf.base = x->offset;
+    gf.m_fastest = 1;
+    KCHK(gemm(false, EPI_FILTER, gf, st));
+    KCHK(topk_merge(cs, ci, nb, 1, CAND_CAP, k, osc + q0 * k, oix + q0 * k, st));
+    hcnt.resize(nb);
+    HIPCHK(hipMemcpyAsync(hcnt.data(), cnt, (size_t)nb * 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    for (int64_t i = 0; i < nb; ++i)
+      if (hcnt[i] > CAND_CAP) overflow.push_back(q0 + i);
+  }
+  x->search_stats[0] += nq - (int64_t)overflow.size();
+  if (!overflow.empty()) {   // rare: a sample that under-estimates theta badly; redo exactly
+    x->search_stats[2] += (int64_t)overflow.size();
+    for (int64_t qi : overflow) {
+      r = search_exact(x, q16 + qi * dim, qinv + qi, 1, k, osc + qi * k, oix + qi * k, st);
+      if (r) return r;
+    }
+  }
+  return CLM_OK;
+}
+
+int clm_index_search(clm_index* x, const void* q, int q_dtype, int64_t nq, int k, float* out_scores,
+                     int64_t* out_idx, void* stream) {
+  if (!x || nq < 0 || (nq > 0 && (!q || !out_scores || !out_idx))) return fail(CLM_E_ARG, "bad argument");
+  if (q_dtype != CLM_F32 && q_dtype != CLM_F16) return fail(CLM_E_ARG, "queries must be f32 or f16");
+  if (k < 1 || k > 1024) return fail(CLM_E_ARG, "k must be in [1, 1024]");
+  if (nq == 0) return CLM_OK;
+  DeviceGuard g(x->dev);
+  hipStream_t st = (hipStream_t)stream;
+  const int dim = (int)x->dim;
+  const int64_t N = x->n;
+  const bool q_dev = is_device_ptr(q);
+  const bool o_dev = is_device_ptr(out_scores) && is_device_ptr(out_idx);
+  const size_t q_src_bytes = (size_t)nq * dim * (q_dtype == CLM_F32 ? 4 : 2);
+  size_t off = 0;
+  auto take = [&](size_t bytes) { size_t o = off; off = round_up(off + bytes, 256); return o; };
+  const size_t o_qsrc = q_dev ? 0 : take(q_src_bytes);
+  const size_t o_q16 = take((size_t)nq * dim * 2);
+  const size_t o_qinv = take((size_t)nq * 4);
+  const size_t o_os = o_dev ? 0 : take((size_t)nq * k * 4);
+  const size_t o_oi = o_dev ? 0 : take((size_t)nq * k * 8);
+  int r = grow(&x->ws, &x->ws_bytes, off);
+  if (r) return r;
+  uint8_t* ws = (uint8_t*)x->ws;
+  const void* qsrc = q;
+  if (!q_dev) {
+    HIPCHK(hipMemcpyAsync(ws + o_qsrc, q, q_src_bytes, hipMemcpyHostToDevice, st));
+    qsrc = ws + o_qsrc;
+  }
+  u16* q16 = (u16*)(ws + o_q16);
+  float* qinv = (float*)(ws + o_qinv);
+  // inverse norms of the SOURCE rows (reference normalises the fp32 query, search.py:93)
+  KCHK(rows_to_f16(qsrc, q_dtype == CLM_F32 ? 0 : 1, nq, dim, q16, qinv, st, 1));
+  float* osc = o_dev ? out_scores : (float*)(ws + o_os);
+  int64_t* oix = o_dev ? out_idx : (int64_t*)(ws + o_oi);
+  // filtered single-pass path when the index is large enough for sampling to pay
+  int64_t S = round_up(std::max<int64_t>(8192, (int64_t)k * N / 256), 256);
+  const char* env = getenv("CLM_SEARCH_EXACT");
+  const bool filtered = !(env && atoi(env)) && k <= 256 && N >= 4 * S && S <= (1 << 18);
+  if (filtered) r = search_filtered(x, q16, qinv, nq, k, S, osc, oix, st);
+  else {
+    r = search_exact(x, q16, qinv, nq, k, osc, oix, st);
+    x->search_stats[1] += nq;
+  }
+  if (r) return r;
   if (!o_dev) {
     HIPCHK(hipMemcpyAsync(out_scores, osc, (size_t)nq * k * 4, hipMemcpyDeviceToHost, st));
     HIPCHK(hipMemcpyAsync(out_idx, oix, (size_t)nq * k * 8, hipMemcpyDeviceToHost, st));
@@ -1088,6 +1200,14 @@ int clm_index_search(clm_index* x, const void* q, int q_dtype, int64_t nq, int k
   } else if (!q_dev) {
     HIPCHK(hipStreamSynchronize(st));
   }
+  return CLM_OK;
+}
+
+int clm_index_stats(const clm_index* x, int64_t* filtered, int64_t* exact, int64_t* overflow) {
+  if (!x) return fail(CLM_E_ARG, "null index");
+  if (filtered) *filtered = x->search_stats[0];
+  if (exact) *exact = x->search_stats[1];
+  if (overflow) *overflow = x->search_stats[2];
   return CLM_OK;
 }
 

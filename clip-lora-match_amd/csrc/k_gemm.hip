@@ -68,7 +68,8 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_kernel(GemmArgs g) {
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int ntn = (g.N + BN - 1) / BN, ntm = (g.M + BM - 1) / BM;
   const int t = xcd_remap(blockIdx.x, ntn * ntm);
-  const int tm = t / ntn, tn = t % ntn;
+  const int tm = g.m_fastest ? t % ntm : t / ntn;
+  const int tn = g.m_fastest ? t / ntm : t % ntn;
   const int m0 = tm * BM, n0 = tn * BN;
 
   // per-lane DMA sources: piece i of this wave covers tile rows (wid*LA + i)*8 .. +8
@@ -148,7 +149,9 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_kernel(GemmArgs g) {
     float rs = 1.f;
     int64_t prow = m;
     const float* aux = nullptr;
-    if constexpr (EPI == EPI_SCORE) rs = g.rscale ? g.rscale[m] : 1.f;
+    if constexpr (EPI == EPI_SCORE || EPI == EPI_FILTER) rs = g.rscale ? g.rscale[m] : 1.f;
+    float th = 0.f;
+    if constexpr (EPI == EPI_FILTER) th = g.theta[(int64_t)m * g.theta_ld];
     if constexpr (EPI == EPI_PATCH) {
       const int b = m / g.group, p = m - b * g.group;
       prow = (int64_t)b * (g.group + 1) + 1 + p;
@@ -183,10 +186,23 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_kernel(GemmArgs g) {
         } else if constexpr (EPI == EPI_PATCH) {
           const float4 p4 = *(const float4*)(aux + n);
           *(float4*)((float*)g.out + prow * g.ldo + n) = make_float4(v[0] + p4.x, v[1] + p4.y, v[2] + p4.z, v[3] + p4.w);
-        } else {  // EPI_SCORE
+        } else if constexpr (EPI == EPI_SCORE) {
           const float4 c4 = g.cscale ? *(const float4*)(g.cscale + n) : make_float4(1.f, 1.f, 1.f, 1.f);
           *(float4*)((float*)g.out + (int64_t)m * g.ldo + n) =
               make_float4(v[0] * rs * c4.x, v[1] * rs * c4.y, v[2] * rs * c4.z, v[3] * rs * c4.w);
+        } else {  // EPI_FILTER
+          const float4 c4 = *(const float4*)(g.cscale + n);
+          const float sc[4] = {v[0] * rs * c4.x, v[1] * rs * c4.y, v[2] * rs * c4.z, v[3] * rs * c4.w};
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            if (sc[j] >= th) {
+              const int slot = atomicAdd(g.cnt + m, 1);
+              if (slot < g.cap) {
+                g.cand_s[(int64_t)m * g.cap + slot] = sc[j];
+                g.cand_i[(int64_t)m * g.cap + slot] = g.base + n + j;
+              }
+            }
+          }
         }
       } else {  // ragged N (not a multiple of 4): scalar tail
 #pragma unroll
@@ -200,7 +216,17 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_kernel(GemmArgs g) {
           else if constexpr (EPI == EPI_GELU) ((u16*)g.out)[(int64_t)m * g.ldo + nj] = from_f32<BF>(quick_gelu(x));
           else if constexpr (EPI == EPI_RESID) ((float*)g.out)[(int64_t)m * g.ldo + nj] += x;
           else if constexpr (EPI == EPI_PATCH) ((float*)g.out)[prow * g.ldo + nj] = x + aux[nj];
-          else ((float*)g.out)[(int64_t)m * g.ldo + nj] = x * rs * (g.cscale ? g.cscale[nj] : 1.f);
+          else if constexpr (EPI == EPI_SCORE) ((float*)g.out)[(int64_t)m * g.ldo + nj] = x * rs * (g.cscale ? g.cscale[nj] : 1.f);
+          else {
+            const float sc = x * rs * g.cscale[nj];
+            if (sc >= th) {
+              const int slot = atomicAdd(g.cnt + m, 1);
+              if (slot < g.cap) {
+                g.cand_s[(int64_t)m * g.cap + slot] = sc;
+                g.cand_i[(int64_t)m * g.cap + slot] = g.base + nj;
+              }
+            }
+          }
         }
       }
     }
@@ -269,6 +295,7 @@ hipError_t dispatch(int epi, int id, const GemmArgs& g, hipStream_t s) {
     case EPI_RESID: return launch_id<BF, EPI_RESID>(id, g, s);
     case EPI_PATCH: return launch_id<BF, EPI_PATCH>(id, g, s);
     case EPI_SCORE: return launch_id<BF, EPI_SCORE>(id, g, s);
+    case EPI_FILTER: return launch_id<BF, EPI_FILTER>(id, g, s);
     default: return hipErrorInvalidValue;
   }
 }

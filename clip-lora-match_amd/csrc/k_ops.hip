@@ -361,6 +361,16 @@ __global__ __launch_bounds__(256) void rows_to_f16_kernel(const void* src, int s
   if (lane == 0) inv_norm[row] = 1.0f / sqrtf(s);
 }
 
+__global__ __launch_bounds__(256) void sample_rows_kernel(const u16* rows, const float* inv, int64_t n, int dim,
+                                                          int64_t S, u16* out_rows, float* out_inv) {
+  const int64_t sidx = blockIdx.x;
+  const int64_t src = sidx * n / S;
+  const uint4* a = (const uint4*)(rows + src * dim);
+  uint4* b = (uint4*)(out_rows + sidx * dim);
+  for (int e = threadIdx.x; e < dim / 8; e += blockDim.x) b[e] = a[e];
+  if (threadIdx.x == 0) out_inv[sidx] = inv[src];
+}
+
 __global__ __launch_bounds__(256) void l2n_kernel(float* rows, int64_t n, int dim) {
   const int lane = threadIdx.x & 63;
   const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -443,6 +453,14 @@ hipError_t rows_to_f16(const void* src, int src_dtype, int64_t n, int dim, u16* 
                        hipStream_t s, int norm_src) {
   if (n <= 0) return hipSuccess;
   rows_to_f16_kernel<<<(unsigned)((n + 3) / 4), 256, 0, s>>>(src, src_dtype, n, dim, dst, inv_norm, norm_src);
+  return hipGetLastError();
+}
+
+hipError_t sample_rows(const u16* rows, const float* inv, int64_t n, int dim, int64_t S, u16* out_rows,
+                       float* out_inv, hipStream_t s) {
+  if (S <= 0) return hipSuccess;
+  if (dim % 8) return hipErrorInvalidValue;
+  sample_rows_kernel<<<(unsigned)S, 64, 0, s>>>(rows, inv, n, dim, S, out_rows, out_inv);
   return hipGetLastError();
 }
 

@@ -12,7 +12,9 @@ enum Epi {
   EPI_GELU = 1,   // out16[m,n] = quick_gelu(acc + bias[n])
   EPI_RESID = 2,  // outf[m,n] += acc + bias[n]            (fp32 residual stream)
   EPI_PATCH = 3,  // outf[b*(G+1)+1+p, n] = acc + aux[(1+p)*aux_ld + n], m = b*G+p
-  EPI_SCORE = 4   // outf[m,n] = acc * rscale[m] * cscale[n]  (cosine scores)
+  EPI_SCORE = 4,  // outf[m,n] = acc * rscale[m] * cscale[n]  (cosine scores)
+  EPI_FILTER = 5  // s = acc*rscale[m]*cscale[n]; if s >= theta[m]: append (s, base+n) to row m's
+                  // candidate list (atomic slot in cnt[m], capacity cap)
 };
 
 struct GemmArgs {
@@ -23,6 +25,9 @@ struct GemmArgs {
   const float* bias;
   const float* aux; int64_t aux_ld; int group;
   const float* rscale; const float* cscale;
+  // EPI_FILTER
+  const float* theta; int64_t theta_ld; int* cnt; float* cand_s; int64_t* cand_i; int cap; int64_t base;
+  int m_fastest;   // tile order: 1 = consecutive workgroups walk M (share one W tile)
 };
 
 hipError_t gemm(bool bf16, int epi, const GemmArgs& g, hipStream_t s);
@@ -89,6 +94,9 @@ hipError_t topk_rows(const float* scores, int64_t lds, int64_t nq, int64_t C, in
 hipError_t topk_merge(const float* in_s, const int64_t* in_i, int64_t nq, int parts, int k_in,
                       int k, float* out_s, int64_t* out_i, hipStream_t s);
 hipError_t l2_normalize_rows(float* rows, int64_t n, int dim, hipStream_t s);
+// strided row sample: out[s] = rows[s * n / S] (fp16 rows + fp32 inverse norms)
+hipError_t sample_rows(const u16* rows, const float* inv, int64_t n, int dim, int64_t S, u16* out_rows,
+                       float* out_inv, hipStream_t s);
 hipError_t f32_to_f16_rows(const float* src, int64_t n, int dim, u16* dst, hipStream_t s);
 
 }  // namespace clm

@@ -102,6 +102,12 @@ class CosineIndex:
                                          C.stream_of(self.device)), "clm_index_search")
         return s, i
 
+    def stats(self) -> dict:
+        """queries served by the single-pass filtered path / the exact path / overflow re-runs"""
+        f, e, o = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
+        C.check(C.lib().clm_index_stats(self._h, ctypes.byref(f), ctypes.byref(e), ctypes.byref(o)))
+        return {"filtered": f.value, "exact": e.value, "overflow": o.value}
+
     def close(self) -> None:
         if getattr(self, "_h", None):
             C.lib().clm_index_destroy(self._h)

@@ -137,6 +137,10 @@ int clm_index_read(clm_index* idx, int64_t start, int64_t n, float* dst, void* s
 int clm_index_search(clm_index* idx, const void* q, int q_dtype, int64_t nq, int k,
                      float* out_scores, int64_t* out_idx, void* stream);
 
+/* search-path counters since creation: queries served by the single-pass filtered path,
+ * by the exact chunked path, and filtered queries redone exactly after a candidate overflow */
+int clm_index_stats(const clm_index* idx, int64_t* filtered, int64_t* exact, int64_t* overflow);
+
 /* full cosine matrix: out [nq, n] f32 = normalise(q) . normalise(c)^T */
 int clm_cosine_scores(int hip_device, const float* q, int64_t nq, const float* c, int64_t n,
                       int dim, float* out, void* stream);

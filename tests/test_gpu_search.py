@@ -157,3 +157,40 @@ def test_large_index_property():
     assert torch.equal(i[:, 0], plant)
     assert torch.all(torch.abs(s[:, 0] - 1) < 1e-3)
     assert torch.all(s[:, 1:] <= s[:, :-1])
+
+
+@pytest.mark.parametrize("k", [1, 5, 64, 256])
+def test_filtered_path_equals_exact_path(k, monkeypatch):
+    """The single-pass threshold-filter search returns exactly what the exact chunked path
+    returns (same scores bit for bit, same indices), and reports which path served."""
+    n, dim, nq = 1_000_000, 512, 96
+    g = torch.Generator(device="cuda").manual_seed(k)
+    rows = torch.randn((n, dim), generator=g, device="cuda").half()
+    q = torch.randn((nq, dim), generator=g, device="cuda").half()
+    idx = CosineIndex(dim, capacity=n)
+    idx.append(rows)
+    s1, i1 = idx.search(q, k)
+    st = idx.stats()
+    assert st["filtered"] == nq and st["exact"] == 0
+    monkeypatch.setenv("CLM_SEARCH_EXACT", "1")
+    s2, i2 = idx.search(q, k)
+    assert idx.stats()["exact"] == nq
+    assert torch.equal(i1, i2) and torch.equal(s1, s2)
+
+
+def test_filtered_path_overflow_falls_back():
+    """300k identical rows make every one of them a candidate (> capacity): those queries
+    are redone exactly and return the k smallest indices of the tie group."""
+    n, dim = 1_000_000, 128
+    g = torch.Generator(device="cuda").manual_seed(3)
+    rows = torch.randn((n, dim), generator=g, device="cuda")
+    dup = torch.randn((dim,), generator=g, device="cuda")
+    pos = torch.randperm(n, generator=g, device="cuda")[:300_000].sort().values
+    rows[pos] = dup
+    idx = CosineIndex(dim, capacity=n)
+    idx.append(rows.half())
+    q = torch.stack([dup, torch.randn((dim,), generator=g, device="cuda")]).half()
+    s, i = idx.search(q, 8)
+    assert idx.stats()["overflow"] >= 1
+    assert torch.equal(i[0], pos[:8])
+    assert torch.all(s[0] > 0.999)
