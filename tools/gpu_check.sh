@@ -19,6 +19,8 @@ for st in $STAGES; do
     sweep)
       timeout -k 10 600 python tools/gemm_sweep.py > gpurun_out/sweep.jsonl 2> gpurun_out/sweep.err
       rc=$?; echo "sweep rc=$rc"; cat gpurun_out/sweep.jsonl | head -80; tail -3 gpurun_out/sweep.err; [ $rc -eq 0 ] || exit $rc ;;
+    pmc)
+      timeout -k 10 1500 bash tools/pmc.sh; rc=$?; echo "pmc rc=$rc"; [ $rc -eq 0 ] || exit $rc ;;
     prof)
       export TMPDIR=/tmp
       timeout -k 10 900 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python bench.py --no-cpu-baseline ${PROF_ARGS:-} > gpurun_out/prof.log 2>&1
