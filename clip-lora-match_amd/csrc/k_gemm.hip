@@ -260,11 +260,16 @@ hipError_t launch_id(int id, const GemmArgs& g, hipStream_t s) {
     case 3: return launch_cfg<BF, EPI, 128, 256, 2, 4, 3>(g, s);
     case 4: return launch_cfg<BF, EPI, 256, 256, 4, 2, 2>(g, s);
     case 5: return launch_cfg<BF, EPI, 64, 128, 1, 2, 3>(g, s);
+    case 6: return launch_cfg<BF, EPI, 128, 192, 2, 2, 2>(g, s);
+    case 7: return launch_cfg<BF, EPI, 192, 128, 2, 2, 2>(g, s);
+    case 8: return launch_cfg<BF, EPI, 256, 128, 4, 2, 2>(g, s);
+    case 9: return launch_cfg<BF, EPI, 192, 192, 2, 2, 2>(g, s);
+    case 10: return launch_cfg<BF, EPI, 128, 256, 2, 4, 2>(g, s);
     default: return hipErrorInvalidValue;
   }
 }
 
-constexpr int NCFG = 6;
+constexpr int NCFG = 11;
 
 // Tile choice (measured, profiles/r01_v2_gemm_sweep.jsonl): the 2-stage 128x128 tile
 // (64 KiB LDS -> 2 workgroups per CU) wins on the encoder's narrow / short-K GEMMs;
