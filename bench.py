@@ -61,6 +61,23 @@ def flops_per_pair(cfg) -> dict:
     return {"image": float(img), "caption": float(txt)}
 
 
+def gemm_algorithmic_bytes(cfg, B) -> float:
+    """Compulsory HBM bytes of one step's GEMMs: A read once, W read once, output written once
+    (fp32 residual read + written for out_proj / fc2), bf16 operands."""
+    tot = 0.0
+    for tw, T in ((cfg.vision, cfg.vision_seq), (cfg.text, cfg.max_pos)):
+        M, d, f = B * T, tw.hidden, tw.mlp
+        per_layer = (M * d * 2 + 3 * d * d * 2 + M * 3 * d * 2        # qkv
+                     + M * d * 2 + d * d * 2 + M * d * 8               # out (+ fp32 residual RMW)
+                     + M * d * 2 + f * d * 2 + M * f * 2               # fc1
+                     + M * f * 2 + d * f * 2 + M * d * 8)              # fc2 (+ residual RMW)
+        tot += tw.layers * per_layer
+    P = B * cfg.num_patches
+    tot += P * cfg.channels * cfg.patch ** 2 * 2 + cfg.vision.hidden * cfg.channels * cfg.patch ** 2 * 2 + \
+        B * cfg.vision_seq * cfg.vision.hidden * 4
+    return tot
+
+
 def cpu_baseline(cfg, sd, lora, budget_s: float):
     """transformers CLIPModel fp32 on the host cores + restated PEFT LoRA (oracle/hf_ref.py)."""
     from oracle import hf_ref as H
@@ -116,6 +133,17 @@ def search_leg(rows: int, queries: int, k: int, device):
             "index_dtype": "fp16", "tflops": flops / dt / 1e12}
 
 
+def pmc_traffic():
+    """HBM bytes per GEMM launch from the newest committed PMC summary (tools/pmc_summary.py),
+    or None when no counter run has been recorded."""
+    import glob
+    files = sorted(glob.glob(os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "*_pmc_summary.json")))
+    if not files:
+        return None, None
+    d = json.load(open(files[-1]))
+    return d.get("gemm_mean_hbm_bytes_per_launch"), os.path.basename(files[-1])
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -157,7 +185,7 @@ def main():
     gathered = torch.empty((world * 2 * B, cfg.proj_dim), dtype=torch.float32, device=dev) if world > 1 else None
 
     def step():
-        if args.sequential:
+        if args.sequential or profiling[0]:   # profiled pass: one stream, so kernel spans don't overlap
             model.encode_pixels(imgs, out=emb[:B])
             model.encode_ids(ids, out=emb[B:])
         else:   # towers concurrently on two streams, replayed from a captured hipGraph
@@ -196,6 +224,8 @@ def main():
     model.prof_enable(False)
     gemm_ms, gemm_flops, gemm_n = prof["gemm"]
     fp = flops_per_pair(cfg)
+    traffic, traffic_src = pmc_traffic()
+    gemm_bytes = gemm_algorithmic_bytes(cfg, B) * nprof
     step_flops = B * (fp["image"] + fp["caption"])
 
     result = {
@@ -225,7 +255,10 @@ def main():
             "peak": MFMA_PEAK_TFLOPS,
             "unit": "TFLOP/s",
             "frac": round(gemm_flops / (gemm_ms * 1e-3) / 1e12 / MFMA_PEAK_TFLOPS, 4),
-            "traffic": None,
+            "traffic": traffic,
+            "traffic_unit": "bytes per launch (PMC: 2*FETCH_SIZE + WRITE_SIZE, gfx950-corrected)",
+            "traffic_source": traffic_src,
+            "algorithmic_bytes_per_launch": round(gemm_bytes / max(gemm_n, 1)),
             "avg_launch_us": round(gemm_ms / gemm_n * 1e3, 2),
             "launches_per_step": gemm_n // nprof,
             "kernel_ms_per_step": {k: round(v[0] / nprof, 4) for k, v in prof.items()},

@@ -68,8 +68,19 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_kernel(GemmArgs g) {
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int ntn = (g.N + BN - 1) / BN, ntm = (g.M + BM - 1) / BM;
   const int t = xcd_remap(blockIdx.x, ntn * ntm);
-  const int tm = g.m_fastest ? t % ntm : t / ntn;
-  const int tn = g.m_fastest ? t / ntm : t % ntn;
+  int tm, tn;
+  if (g.m_fastest) {          // every query tile of one index tile back to back (search)
+    tm = t % ntm;
+    tn = t / ntm;
+  } else {                    // grouped raster: GM row-panels x all N-tiles per group, M inner,
+    constexpr int GM = 8;     // so an XCD's concurrent tiles share A panels and W tiles in L2
+    const int group = t / (GM * ntn);
+    const int first_m = group * GM;
+    const int gsz = min(GM, ntm - first_m);
+    const int r = t - group * GM * ntn;
+    tm = first_m + r % gsz;
+    tn = r / gsz;
+  }
   const int m0 = tm * BM, n0 = tn * BN;
 
   // per-lane DMA sources: piece i of this wave covers tile rows (wid*LA + i)*8 .. +8
@@ -271,11 +282,15 @@ hipError_t launch_id(int id, const GemmArgs& g, hipStream_t s) {
 
 constexpr int NCFG = 11;
 
-// Tile choice (measured, profiles/r01_v2_gemm_sweep.jsonl): the 2-stage 128x128 tile
-// (64 KiB LDS -> 2 workgroups per CU) wins on the encoder's narrow / short-K GEMMs;
-// the 256x256 tile (1 workgroup per CU) wins when its tile count fills the last
-// round of 256 CUs well (qkv: 1.76-1.80 rounds; square 4096^3: 1.0), and loses when
-// a mostly-empty last round remains (fc1: 2.3-2.4 rounds). $CLM_GEMM_CFG overrides.
+// Tile choice: a cost model calibrated on the sweep (profiles/r01_v3_gemm_sweep.jsonl).
+// time(cfg) ~ rounds(cfg) x round_cost(cfg), rounds = ceil(tiles / resident workgroups),
+// round_cost = BM*BN*(workgroups per CU) / efficiency(cfg) with the efficiencies measured on
+// 4096^3 (bf16, TF/s / 1000). Narrow GEMMs (N = 512, 768) pick 192x128 (one round instead of
+// two 128x128 rounds); wide ones pick 256x256 or 256x128 / 128x256. $CLM_GEMM_CFG overrides.
+struct CfgModel { int id, bm, bn, wg_per_cu; double eff; };
+constexpr CfgModel MODELS[] = {
+  {0, 128, 128, 2, 0.975}, {4, 256, 256, 1, 1.18}, {6, 128, 192, 2, 0.955}, {7, 192, 128, 2, 0.955},
+  {8, 256, 128, 1, 1.025}, {10, 128, 256, 1, 1.056}};
 int pick_config(int M, int N) {
   static int forced = -2;
   if (forced == -2) {
@@ -283,13 +298,16 @@ int pick_config(int M, int N) {
     forced = e ? atoi(e) : -1;
   }
   if (forced >= 0 && forced < NCFG) return forced;
-  const int64_t t256 = (int64_t)((M + 255) / 256) * ((N + 255) / 256);
-  if (N >= 1024 && t256 >= 256) {
-    const double rounds = t256 / 256.0;
-    const double frac = rounds - (int64_t)rounds;
-    if (frac == 0.0 || frac >= 0.7) return 4;
+  int best = 0;
+  double best_cost = 1e300;
+  for (const CfgModel& c : MODELS) {
+    const int64_t tiles = (int64_t)((M + c.bm - 1) / c.bm) * ((N + c.bn - 1) / c.bn);
+    const int64_t slots = 256LL * c.wg_per_cu;
+    const int64_t rounds = (tiles + slots - 1) / slots;
+    const double cost = rounds * (double)c.bm * c.bn * c.wg_per_cu / c.eff;
+    if (cost < best_cost * 0.999) { best_cost = cost; best = c.id; }
   }
-  return 0;
+  return best;
 }
 
 template <bool BF>

@@ -159,7 +159,7 @@ def test_large_index_property():
     assert torch.all(s[:, 1:] <= s[:, :-1])
 
 
-@pytest.mark.parametrize("k", [1, 5, 64, 256])
+@pytest.mark.parametrize("k", [1, 5, 16, 48])
 def test_filtered_path_equals_exact_path(k, monkeypatch):
     """The single-pass threshold-filter search returns exactly what the exact chunked path
     returns (same scores bit for bit, same indices), and reports which path served."""
@@ -176,6 +176,9 @@ def test_filtered_path_equals_exact_path(k, monkeypatch):
     s2, i2 = idx.search(q, k)
     assert idx.stats()["exact"] == nq
     assert torch.equal(i1, i2) and torch.equal(s1, s2)
+    monkeypatch.delenv("CLM_SEARCH_EXACT")
+    idx.search(q, 256)                    # k*N/256 > N/4: sampling would not pay -> exact path
+    assert idx.stats()["exact"] == 2 * nq
 
 
 def test_filtered_path_overflow_falls_back():
