@@ -19,6 +19,8 @@ for st in $STAGES; do
     sweep)
       timeout -k 10 600 python tools/gemm_sweep.py > gpurun_out/sweep.jsonl 2> gpurun_out/sweep.err
       rc=$?; echo "sweep rc=$rc"; cat gpurun_out/sweep.jsonl | head -80; tail -3 gpurun_out/sweep.err; [ $rc -eq 0 ] || exit $rc ;;
+    stalls)
+      timeout -k 10 1200 bash tools/gemm_stalls.sh; rc=$?; echo "stalls rc=$rc"; [ $rc -eq 0 ] || exit $rc ;;
     pmc)
       timeout -k 10 1500 bash tools/pmc.sh; rc=$?; echo "pmc rc=$rc"; [ $rc -eq 0 ] || exit $rc ;;
     prof)
