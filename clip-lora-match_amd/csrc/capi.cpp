@@ -588,6 +588,8 @@ int clm_gemm(int hip_device, int dtype, int epilogue, int config, const void* A,
   GemmArgs a{};
   a.A = (const u16*)A; a.lda = lda; a.W = (const u16*)W; a.ldw = ldw; a.M = M; a.N = N; a.K = K;
   a.out = out; a.ldo = ldo; a.bias = bias; a.rscale = rscale; a.cscale = cscale;
+  static const int dbg = getenv("CLM_GEMM_DEBUG") ? atoi(getenv("CLM_GEMM_DEBUG")) : 0;
+  a.debug = dbg;
   hipError_t e = gemm_cfg(dtype == CLM_BF16, epilogue, config, a, (hipStream_t)stream);
   if (e != hipSuccess) return fail(CLM_E_HIP, std::string("gemm: ") + hipGetErrorString(e));
   return CLM_OK;

@@ -151,6 +151,13 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_kernel(GemmArgs g) {
     }
   }
 
+  if (g.debug & 1) {   // timing diagnostic: main loop only
+#pragma unroll
+    for (int mb = 0; mb < C::TM; ++mb)
+#pragma unroll
+      for (int nb = 0; nb < C::TN; ++nb) asm volatile("" ::"v"(acc[mb][nb]));
+    return;
+  }
   // ---- epilogue: lane owns C[m, n..n+3], m = ...+(lane&15), n = ...+(lane>>4)*4 ----
   const bool nvec = (g.N % 4) == 0 && (g.ldo % 4) == 0;
 #pragma unroll

@@ -19,6 +19,9 @@ for st in $STAGES; do
     sweep)
       timeout -k 10 600 python tools/gemm_sweep.py > gpurun_out/sweep.jsonl 2> gpurun_out/sweep.err
       rc=$?; echo "sweep rc=$rc"; cat gpurun_out/sweep.jsonl | head -80; tail -3 gpurun_out/sweep.err; [ $rc -eq 0 ] || exit $rc ;;
+    split)
+      timeout -k 10 600 python tools/gemm_split.py > gpurun_out/split.jsonl 2> gpurun_out/split.err
+      rc=$?; echo "split rc=$rc"; cat gpurun_out/split.jsonl; tail -3 gpurun_out/split.err; [ $rc -eq 0 ] || exit $rc ;;
     stalls)
       timeout -k 10 1200 bash tools/gemm_stalls.sh; rc=$?; echo "stalls rc=$rc"; [ $rc -eq 0 ] || exit $rc ;;
     pmc)
