@@ -158,6 +158,7 @@ def main():
     ap.add_argument("--search-queries", type=int, default=10_000)
     ap.add_argument("--no-search", action="store_true")
     ap.add_argument("--sequential", action="store_true", help="towers back to back on one stream, no graph")
+    ap.add_argument("--split", type=int, default=0, help="sub-batches per tower in encode_pair (0 = library default)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -189,7 +190,8 @@ def main():
             model.encode_pixels(imgs, out=emb[:B])
             model.encode_ids(ids, out=emb[B:])
         else:   # towers concurrently on two streams, replayed from a captured hipGraph
-            model.encode_pair(imgs, ids, out_img=emb[:B], out_txt=emb[B:], graph=not profiling[0])
+            model.encode_pair(imgs, ids, out_img=emb[:B], out_txt=emb[B:], graph=not profiling[0],
+                               split=args.split)
         if world > 1:
             torch.distributed.all_gather_into_tensor(gathered, emb)
 
@@ -242,7 +244,8 @@ def main():
         "dtype": "bf16" if args.dtype == "bfloat16" else "fp16",
         "data": "synthetic (seeded uint8 224x224 RGB images, 77-token id captions; deterministic synthetic weights)",
         "config": {"workload": "ViT-B/32 + LoRA r=8 alpha=16 (q,k,v,out, both towers) encode + L2-normalise",
-                   "execution": "sequential" if args.sequential else "2 streams + hipGraph replay",
+                   "execution": "sequential" if args.sequential else
+                       f"towers x sub-batches on streams (split={args.split or 'auto'}) + hipGraph replay",
                    "per_gpu_batch": B, "global_batch": world * B, "seq_len": cfg.max_pos,
                    "image_size": cfg.image_size, "lora_mode": args.lora_mode,
                    "parallelism": f"dp{world}" + (" + all_gather(embeddings)" if world > 1 else "")},

@@ -142,9 +142,14 @@ struct clm_ctx {
   void* stage_out = nullptr; size_t stage_out_bytes = 0;
   int32_t* ids_dev = nullptr;
   // two-tower concurrency + graph replay (clm_encode_pair)
-  hipStream_t s_img = nullptr, s_txt = nullptr;
-  hipEvent_t ev_fork = nullptr, ev_txt = nullptr, ev_done = nullptr;
-  typedef std::tuple<const void*, int, int, const void*, int, int, void*, void*, int, int> PairKey;
+  // Each tower's batch is cut into `split` sub-batches on their own streams (disjoint row
+  // ranges of the tower workspace): one sub-batch's write-bound GEMM epilogues and
+  // latency-bound LN/attention launches overlap another's MFMA main loops.
+  static constexpr int MAX_SPLIT = 4;
+  hipStream_t ps[2 * MAX_SPLIT] = {};
+  hipEvent_t pev[2 * MAX_SPLIT] = {};
+  hipEvent_t ev_fork = nullptr, ev_done = nullptr;
+  typedef std::tuple<const void*, int, int, const void*, int, int, void*, void*, int, int, int> PairKey;
   std::map<PairKey, hipGraphExec_t> graphs;
   // kernel timing (clm_prof_*): events recorded on the launch stream
   bool prof = false;
@@ -515,10 +520,19 @@ int run_layers(clm_ctx* c, Tower& T, int B, int S, bool causal, hipStream_t st) 
   return CLM_OK;
 }
 
-int encode_image_chunk(clm_ctx* c, const void* pix, int layout, int B, void* out, int out_dtype, int normalize,
-                       hipStream_t st) {
+// the tower with its workspace pointers moved to sub-batch b0 (items of `rows` sequence rows)
+Tower ws_view(const Tower& T0, int b0, int rows, int patches, int proj_dim) {
+  Tower T = T0;
+  const int64_t r0 = (int64_t)b0 * rows;
+  T.h += r0 * T.d; T.X += r0 * T.ldx; T.QKV += r0 * 3 * T.d; T.O += r0 * T.ldo; T.Hm += r0 * T.ldm;
+  if (T.P) T.P += (int64_t)b0 * patches * T.kp;
+  T.pooled += (int64_t)b0 * proj_dim;
+  return T;
+}
+
+int encode_image_chunk(clm_ctx* c, Tower& T, const void* pix, int layout, int B, void* out, int out_dtype,
+                       int normalize, hipStream_t st) {
   const clm_model_desc& d = c->desc;
-  Tower& T = c->vis;
   const bool bf = c->bf16();
   const int G = d.image_size / d.patch, Tn = G * G + 1;
   { PROF(CLM_PROF_OTHER, (double)B * G * G * T.kp * 2.0 + (double)B * d.image_size * d.image_size * d.channels);
@@ -539,10 +553,9 @@ int encode_image_chunk(clm_ctx* c, const void* pix, int layout, int B, void* out
   return CLM_OK;
 }
 
-int encode_text_chunk(clm_ctx* c, const int32_t* ids_dev, int B, int L, void* out, int out_dtype, int normalize,
-                      hipStream_t st) {
+int encode_text_chunk(clm_ctx* c, Tower& T, const int32_t* ids_dev, int B, int L, void* out, int out_dtype,
+                      int normalize, hipStream_t st) {
   const clm_model_desc& d = c->desc;
-  Tower& T = c->txt;
   const bool bf = c->bf16();
   LnArgs a{};
   a.mode = 1; a.ids = ids_dev; a.tok = T.tok; a.pos = T.tpos; a.L = L;
@@ -663,10 +676,12 @@ int clm_ctx_destroy(clm_ctx* ctx) {
   (void)hipDeviceSynchronize();
   ctx->free_all();
   for (hipEvent_t e : ctx->ev_pool) (void)hipEventDestroy(e);
-  for (hipEvent_t e : {ctx->ev_fork, ctx->ev_txt, ctx->ev_done})
+  for (hipEvent_t e : {ctx->ev_fork, ctx->ev_done})
     if (e) (void)hipEventDestroy(e);
-  for (hipStream_t q : {ctx->s_img, ctx->s_txt})
-    if (q) (void)hipStreamDestroy(q);
+  for (int i = 0; i < 2 * clm_ctx::MAX_SPLIT; ++i) {
+    if (ctx->pev[i]) (void)hipEventDestroy(ctx->pev[i]);
+    if (ctx->ps[i]) (void)hipStreamDestroy(ctx->ps[i]);
+  }
   delete ctx;
   return CLM_OK;
 }
@@ -752,7 +767,7 @@ int clm_encode_image(clm_ctx* ctx, const void* pixels, int pix_layout, int n, vo
       src = ctx->stage_in;
     }
     void* dst = out_dev ? (void*)((uint8_t*)out + (size_t)i0 * out_row) : ctx->stage_out;
-    int r = encode_image_chunk(ctx, src, pix_layout, B, dst, out_dtype, normalize, st);
+    int r = encode_image_chunk(ctx, ctx->vis, src, pix_layout, B, dst, out_dtype, normalize, st);
     if (r) return r;
     if (!out_dev) {
       HIPCHK(hipMemcpyAsync((uint8_t*)out + (size_t)i0 * out_row, ctx->stage_out, out_row * B, hipMemcpyDeviceToHost, st));
@@ -793,7 +808,7 @@ int clm_encode_text(clm_ctx* ctx, const int32_t* ids, int n, int L, void* out, i
       src = ctx->ids_dev;
     }
     void* dst = out_dev ? (void*)((uint8_t*)out + (size_t)i0 * out_row) : ctx->stage_out;
-    int r = encode_text_chunk(ctx, src, B, L, dst, out_dtype, normalize, st);
+    int r = encode_text_chunk(ctx, ctx->txt, src, B, L, dst, out_dtype, normalize, st);
     if (r) return r;
     if (!out_dev) {
       HIPCHK(hipMemcpyAsync((uint8_t*)out + (size_t)i0 * out_row, ctx->stage_out, out_row * B, hipMemcpyDeviceToHost, st));
@@ -805,17 +820,36 @@ int clm_encode_text(clm_ctx* ctx, const int32_t* ids, int n, int L, void* out, i
   return CLM_OK;
 }
 
-static int pair_launch(clm_ctx* c, const void* pixels, int layout, int n_img, const int32_t* ids, int n_txt,
-                       int L, void* oi, void* ot, int out_dtype, int normalize) {
-  // fork: both tower streams wait on ev_fork (recorded on the origin stream by the caller)
-  HIPCHK(hipStreamWaitEvent(c->s_img, c->ev_fork, 0));
-  HIPCHK(hipStreamWaitEvent(c->s_txt, c->ev_fork, 0));
-  int r = n_img ? encode_image_chunk(c, pixels, layout, n_img, oi, out_dtype, normalize, c->s_img) : CLM_OK;
-  if (r) return r;
-  r = n_txt ? encode_text_chunk(c, ids, n_txt, L, ot, out_dtype, normalize, c->s_txt) : CLM_OK;
-  if (r) return r;
-  HIPCHK(hipEventRecord(c->ev_txt, c->s_txt));
-  HIPCHK(hipStreamWaitEvent(c->s_img, c->ev_txt, 0));   // join on s_img
+// Sub-batch launches of one encode_pair on ps[0..2*split): images on ps[2j], captions on
+// ps[2j+1]. `fork` has been recorded on ps[0]; every other stream waits on it, and ps[0]
+// waits on every other stream's pev at the end (join).
+static int pair_launch(clm_ctx* c, int split, hipEvent_t fork, const void* pixels, int layout, int n_img,
+                       const int32_t* ids, int n_txt, int L, void* oi, void* ot, int out_dtype, int normalize) {
+  const clm_model_desc& d = c->desc;
+  const int G = d.image_size / d.patch, Tn = G * G + 1;
+  const size_t pix_bytes = (size_t)d.image_size * d.image_size * d.channels * (layout == CLM_PIX_U8_HWC ? 1 : 4);
+  const size_t out_row = (size_t)d.proj_dim * dtype_size(out_dtype);
+  for (int i = 1; i < 2 * split; ++i) HIPCHK(hipStreamWaitEvent(c->ps[i], fork, 0));
+  for (int j = 0; j < split; ++j) {
+    const int i0 = (int)((int64_t)n_img * j / split), i1 = (int)((int64_t)n_img * (j + 1) / split);
+    const int t0 = (int)((int64_t)n_txt * j / split), t1 = (int)((int64_t)n_txt * (j + 1) / split);
+    if (i1 > i0) {
+      Tower T = ws_view(c->vis, i0, Tn, G * G, d.proj_dim);
+      int r = encode_image_chunk(c, T, (const uint8_t*)pixels + i0 * pix_bytes, layout, i1 - i0,
+                                 (uint8_t*)oi + i0 * out_row, out_dtype, normalize, c->ps[2 * j]);
+      if (r) return r;
+    }
+    if (t1 > t0) {
+      Tower T = ws_view(c->txt, t0, L, 0, d.proj_dim);
+      int r = encode_text_chunk(c, T, ids + (int64_t)t0 * L, t1 - t0, L, (uint8_t*)ot + t0 * out_row, out_dtype,
+                                normalize, c->ps[2 * j + 1]);
+      if (r) return r;
+    }
+  }
+  for (int i = 1; i < 2 * split; ++i) {
+    HIPCHK(hipEventRecord(c->pev[i], c->ps[i]));
+    HIPCHK(hipStreamWaitEvent(c->ps[0], c->pev[i], 0));
+  }
   return CLM_OK;
 }
 
@@ -835,52 +869,54 @@ int clm_encode_pair(clm_ctx* ctx, const void* pixels, int pix_layout, int n_img,
   if (n_img == 0 && n_txt == 0) return CLM_OK;
   DeviceGuard g(ctx->dev);
   hipStream_t st = (hipStream_t)stream;
-  if (!ctx->s_img) {
-    HIPCHK(hipStreamCreateWithFlags(&ctx->s_img, hipStreamNonBlocking));
-    HIPCHK(hipStreamCreateWithFlags(&ctx->s_txt, hipStreamNonBlocking));
+  if (!ctx->ps[0]) {
+    for (int i = 0; i < 2 * clm_ctx::MAX_SPLIT; ++i) {
+      HIPCHK(hipStreamCreateWithFlags(&ctx->ps[i], hipStreamNonBlocking));
+      HIPCHK(hipEventCreateWithFlags(&ctx->pev[i], hipEventDisableTiming));
+    }
     HIPCHK(hipEventCreateWithFlags(&ctx->ev_fork, hipEventDisableTiming));
-    HIPCHK(hipEventCreateWithFlags(&ctx->ev_txt, hipEventDisableTiming));
     HIPCHK(hipEventCreateWithFlags(&ctx->ev_done, hipEventDisableTiming));
   }
+  // sub-batches per tower: flags, else CLM_PAIR_SPLIT, else by batch size
+  static const int env_split = getenv("CLM_PAIR_SPLIT") ? atoi(getenv("CLM_PAIR_SPLIT")) : 0;
+  int split = (flags >> CLM_PAIR_SPLIT_SHIFT) & 15;
+  if (!split) split = env_split > 0 ? env_split : (std::max(n_img, n_txt) >= 128 ? 2 : 1);
+  split = std::max(1, std::min({split, clm_ctx::MAX_SPLIT, std::max(n_img, n_txt)}));
   const bool use_graph = (flags & CLM_PAIR_GRAPH) && !ctx->prof;
   HIPCHK(hipEventRecord(ctx->ev_fork, st));
+  HIPCHK(hipStreamWaitEvent(ctx->ps[0], ctx->ev_fork, 0));
   if (!use_graph) {
-    int r = pair_launch(ctx, pixels, pix_layout, n_img, ids, n_txt, L, out_img, out_txt, out_dtype, normalize);
+    int r = pair_launch(ctx, split, ctx->ev_fork, pixels, pix_layout, n_img, ids, n_txt, L, out_img, out_txt,
+                        out_dtype, normalize);
     if (r) return r;
   } else {
-    clm_ctx::PairKey key(pixels, pix_layout, n_img, ids, n_txt, L, out_img, out_txt, out_dtype, normalize);
+    clm_ctx::PairKey key(pixels, pix_layout, n_img, ids, n_txt, L, out_img, out_txt, out_dtype, normalize, split);
     auto it = ctx->graphs.find(key);
     if (it == ctx->graphs.end()) {
       if (ctx->graphs.size() >= 16) ctx->drop_graphs();
-      // capture on s_img; the fork edge is the wait on ev_fork recorded outside the capture,
-      // so capture starts after it: wait first, then capture the pure kernel sequence
-      HIPCHK(hipStreamWaitEvent(ctx->s_img, ctx->ev_fork, 0));
-      HIPCHK(hipStreamBeginCapture(ctx->s_img, hipStreamCaptureModeRelaxed));
-      HIPCHK(hipEventRecord(ctx->ev_done, ctx->s_img));            // in-capture fork point
-      HIPCHK(hipStreamWaitEvent(ctx->s_txt, ctx->ev_done, 0));
-      int r = n_img ? encode_image_chunk(ctx, pixels, pix_layout, n_img, out_img, out_dtype, normalize, ctx->s_img)
-                    : CLM_OK;
-      if (!r && n_txt) r = encode_text_chunk(ctx, ids, n_txt, L, out_txt, out_dtype, normalize, ctx->s_txt);
-      hipError_t e1 = hipEventRecord(ctx->ev_txt, ctx->s_txt);
-      hipError_t e2 = hipStreamWaitEvent(ctx->s_img, ctx->ev_txt, 0);
+      // capture the pure kernel DAG on ps[0]; the fork edge from the origin stream is the
+      // wait on ev_fork above (outside the capture); inside, ev_done is the fork point
+      HIPCHK(hipStreamBeginCapture(ctx->ps[0], hipStreamCaptureModeRelaxed));
+      hipError_t e1 = hipEventRecord(ctx->ev_done, ctx->ps[0]);
+      int r = e1 == hipSuccess ? pair_launch(ctx, split, ctx->ev_done, pixels, pix_layout, n_img, ids, n_txt, L,
+                                             out_img, out_txt, out_dtype, normalize)
+                               : CLM_OK;
       hipGraph_t graph = nullptr;
-      hipError_t e3 = hipStreamEndCapture(ctx->s_img, &graph);
+      hipError_t e3 = hipStreamEndCapture(ctx->ps[0], &graph);
       if (r) { if (graph) (void)hipGraphDestroy(graph); return r; }
-      if (e1 != hipSuccess || e2 != hipSuccess || e3 != hipSuccess) {
+      if (e1 != hipSuccess || e3 != hipSuccess) {
         if (graph) (void)hipGraphDestroy(graph);
-        return fail(CLM_E_HIP, std::string("graph capture: ") + hipGetErrorString(e3 != hipSuccess ? e3 : (e1 != hipSuccess ? e1 : e2)));
+        return fail(CLM_E_HIP, std::string("graph capture: ") + hipGetErrorString(e3 != hipSuccess ? e3 : e1));
       }
       hipGraphExec_t exec = nullptr;
       hipError_t e4 = hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0);
       (void)hipGraphDestroy(graph);
       if (e4 != hipSuccess) return fail(CLM_E_HIP, std::string("graph instantiate: ") + hipGetErrorString(e4));
       it = ctx->graphs.emplace(key, exec).first;
-    } else {
-      HIPCHK(hipStreamWaitEvent(ctx->s_img, ctx->ev_fork, 0));
     }
-    HIPCHK(hipGraphLaunch(it->second, ctx->s_img));
+    HIPCHK(hipGraphLaunch(it->second, ctx->ps[0]));
   }
-  HIPCHK(hipEventRecord(ctx->ev_done, ctx->s_img));
+  HIPCHK(hipEventRecord(ctx->ev_done, ctx->ps[0]));
   HIPCHK(hipStreamWaitEvent(st, ctx->ev_done, 0));
   return CLM_OK;
 }

@@ -60,91 +60,6 @@ __device__ __forceinline__ void lds_barrier() {
   asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
 
-// Output element type of an epilogue (bf16/f16 for STORE/GELU, fp32 otherwise)
-template <int EPI> constexpr int out_bytes() { return (EPI == EPI_STORE || EPI == EPI_GELU) ? 2 : 4; }
-
-template <bool BF, int EPI, int BM, int BN, int WM, int WN, int STAGES, int TM, int TN>
-__device__ __forceinline__ void epilogue_staged(const GemmArgs& g, f32x4 (&acc)[TM][TN], uint8_t* smem, int m0,
-                                                int n0, int wm, int wn, int lane) {
-  constexpr int EB = out_bytes<EPI>();
-  constexpr int RB = BM / WM;                    // rows per band
-  constexpr int ROWB = BN * EB + 16;             // LDS row stride (+16 B: rotates banks per row)
-  constexpr int CPR = BN * EB / 16;              // 16-B chunks per row
-  constexpr int NT = WM * WN * 64;
-  static_assert(RB * ROWB <= STAGES * (BM + BN) * 128, "band does not fit the LDS");
-  const int tid = threadIdx.x;
-  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");   // operand reads finished
-#pragma unroll
-  for (int band = 0; band < WM; ++band) {
-    if (wm == band) {
-#pragma unroll
-      for (int mb = 0; mb < TM; ++mb) {
-        const int r = mb * 16 + (lane & 15);                    // row within the band
-        const int m = m0 + band * RB + r;
-        float rs = 1.f;
-        if constexpr (EPI == EPI_SCORE) rs = (g.rscale && m < g.M) ? g.rscale[m] : 1.f;
-#pragma unroll
-        for (int nb = 0; nb < TN; ++nb) {
-          const int c = wn * (BN / WN) + nb * 16 + (lane >> 4) * 4;   // column within the tile
-          const int n = n0 + c;
-          float v[4] = {acc[mb][nb][0], acc[mb][nb][1], acc[mb][nb][2], acc[mb][nb][3]};
-          if constexpr (EPI == EPI_STORE || EPI == EPI_GELU || EPI == EPI_RESID) {
-            if (g.bias && n < g.N) {
-              const float4 b4 = *(const float4*)(g.bias + n);
-              v[0] += b4.x; v[1] += b4.y; v[2] += b4.z; v[3] += b4.w;
-            }
-          }
-          if constexpr (EPI == EPI_GELU) {
-#pragma unroll
-            for (int j = 0; j < 4; ++j) v[j] = quick_gelu(v[j]);
-          }
-          if constexpr (EPI == EPI_SCORE) {
-            const float4 c4 = (g.cscale && n < g.N) ? *(const float4*)(g.cscale + n) : make_float4(1.f, 1.f, 1.f, 1.f);
-            v[0] *= rs * c4.x; v[1] *= rs * c4.y; v[2] *= rs * c4.z; v[3] *= rs * c4.w;
-          }
-          uint8_t* dst = smem + r * ROWB + c * EB;
-          if constexpr (EB == 2) {
-            uint2 o;
-            o.x = pack2<BF>(v[0], v[1]);
-            o.y = pack2<BF>(v[2], v[3]);
-            *(uint2*)dst = o;
-          } else {
-            *(float4*)dst = make_float4(v[0], v[1], v[2], v[3]);
-          }
-        }
-      }
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    for (int q = tid; q < RB * CPR; q += NT) {
-      const int r = q / CPR, ch = q - r * CPR;
-      const int m = m0 + band * RB + r;
-      const int n = n0 + ch * (16 / EB);
-      if (m >= g.M || n >= g.N) continue;
-      const uint4 val = *(const uint4*)(smem + r * ROWB + ch * 16);
-      if constexpr (EB == 2) {
-        *(uint4*)((u16*)g.out + (int64_t)m * g.ldo + n) = val;
-      } else {
-        float4 f = __builtin_bit_cast(float4, val);
-        if constexpr (EPI == EPI_RESID) {
-          float4* o = (float4*)((float*)g.out + (int64_t)m * g.ldo + n);
-          const float4 h = *o;
-          f.x += h.x; f.y += h.y; f.z += h.z; f.w += h.w;
-          *o = f;
-        } else if constexpr (EPI == EPI_PATCH) {
-          const int b = m / g.group, p = m - b * g.group;
-          const int64_t prow = (int64_t)b * (g.group + 1) + 1 + p;
-          const float4 p4 = *(const float4*)(g.aux + (int64_t)(1 + p) * g.aux_ld + n);
-          f.x += p4.x; f.y += p4.y; f.z += p4.z; f.w += p4.w;
-          *(float4*)((float*)g.out + prow * g.ldo + n) = f;
-        } else {   // EPI_SCORE
-          *(float4*)((float*)g.out + (int64_t)m * g.ldo + n) = f;
-        }
-      }
-    }
-    if (band + 1 < WM) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-  }
-}
-
 template <bool BF, int EPI, int BM, int BN, int WM, int WN, int STAGES>
 __global__ __launch_bounds__(WM * WN * 64) void gemm_kernel(GemmArgs g) {
   using C = Cfg<BM, BN, WM, WN, STAGES>;
@@ -243,16 +158,9 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_kernel(GemmArgs g) {
       for (int nb = 0; nb < C::TN; ++nb) asm volatile("" ::"v"(acc[mb][nb]));
     return;
   }
-  // ---- staged epilogue: the operand LDS is free now; one wave-row band (BM/WM rows x BN)
-  // at a time goes registers -> LDS, then every wave stores whole contiguous rows with
-  // 16-B lanes (full 128-B lines) instead of 32-B pieces scattered over 16 rows ----
-  if constexpr (EPI != EPI_FILTER) {
-    if ((g.N % 8) == 0 && (g.ldo % 8) == 0) {
-      epilogue_staged<BF, EPI, BM, BN, WM, WN, STAGES>(g, acc, smem, m0, n0, wm, wn, lane);
-      return;
-    }
-  }
-  // ---- direct epilogue: lane owns C[m, n..n+3], m = ...+(lane&15), n = ...+(lane>>4)*4 ----
+  // ---- epilogue (an LDS-staged full-row variant measured slower on every encoder
+  // shape, profiles/r01_v5_gemm_split.jsonl: the cost is the synchronized write burst,
+  // not store coalescing): lane owns C[m, n..n+3], m = ...+(lane&15), n = ...+(lane>>4)*4 ----
   const bool nvec = (g.N % 4) == 0 && (g.ldo % 4) == 0;
 #pragma unroll
   for (int mb = 0; mb < C::TM; ++mb) {

@@ -128,9 +128,12 @@ class ClipLoraModel:
 
     def encode_pair(self, pixels: torch.Tensor, ids: torch.Tensor, normalize: bool = True,
                     out_dtype=torch.float32, out_img: Optional[torch.Tensor] = None,
-                    out_txt: Optional[torch.Tensor] = None, graph: bool = True):
-        """Image batch + caption batch (device tensors, each <= max_batch) encoded concurrently on
-        two streams; graph=True replays a captured hipGraph for repeated identical calls."""
+                    out_txt: Optional[torch.Tensor] = None, graph: bool = True, split: int = 0):
+        """Image batch + caption batch (device tensors, each <= max_batch) encoded concurrently:
+        each tower cut into `split` sub-batches (0 = library default), all pieces on their own
+        streams; graph=True replays a captured hipGraph for repeated identical calls."""
+        if not 0 <= int(split) <= 15:
+            raise ValueError("split must be in [0, 15]")
         S = self.cfg.image_size
         if pixels.dtype == torch.uint8 and tuple(pixels.shape[1:]) == (S, S, self.cfg.channels):
             layout = C.CLM_PIX_U8_HWC
@@ -148,7 +151,8 @@ class ClipLoraModel:
         code = C.CLM_F32 if out_dtype == torch.float32 else C.CLM_F16
         C.check(C.lib().clm_encode_pair(self._ctx, C.ptr(pixels), layout, pixels.shape[0], C.ptr(ids),
                                         ids.shape[0], ids.shape[1], C.ptr(oi), C.ptr(ot), code, int(normalize),
-                                        C.CLM_PAIR_GRAPH if graph else 0, C.stream_of(self.device)),
+                                        (C.CLM_PAIR_GRAPH if graph else 0) | (int(split) << C.CLM_PAIR_SPLIT_SHIFT),
+                                        C.stream_of(self.device)),
                 "clm_encode_pair")
         return oi, ot
 

@@ -110,11 +110,13 @@ int clm_encode_text(clm_ctx* ctx, const int32_t* ids, int n, int L, void* out, i
                     int normalize, void* stream);
 
 /* One image batch and one caption batch (each <= max_batch, device pointers) encoded
- * concurrently: the towers run on two context-owned streams forked from / joined to
- * `stream` with events. flags & CLM_PAIR_GRAPH: the whole launch sequence is captured
- * once per (pointers, shapes) into a hipGraph and replayed on later calls. Results are
- * identical to clm_encode_image + clm_encode_text. */
-enum { CLM_PAIR_GRAPH = 1 };
+ * concurrently: each tower's batch is cut into S sub-batches, and the 2*S pieces run on
+ * context-owned streams forked from / joined to `stream` with events.
+ * flags & CLM_PAIR_GRAPH: the whole launch DAG is captured once per (pointers, shapes, S)
+ * into a hipGraph and replayed on later calls. S = (flags >> CLM_PAIR_SPLIT_SHIFT) & 15,
+ * clamped to [1, 4]; 0 = env CLM_PAIR_SPLIT, else 2 when a tower has >= 128 items, else 1.
+ * Results are identical (bit for bit) to clm_encode_image + clm_encode_text. */
+enum { CLM_PAIR_GRAPH = 1, CLM_PAIR_SPLIT_SHIFT = 8 };
 int clm_encode_pair(clm_ctx* ctx, const void* pixels, int pix_layout, int n_img, const int32_t* ids,
                     int n_txt, int L, void* out_img, void* out_txt, int out_dtype, int normalize,
                     int flags, void* stream);

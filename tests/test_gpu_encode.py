@@ -153,7 +153,8 @@ def test_bad_inputs_raise():
 
 
 @pytest.mark.parametrize("graph", [False, True])
-def test_encode_pair_matches_separate(graph):
+@pytest.mark.parametrize("split", [1, 2, 3])
+def test_encode_pair_matches_separate(graph, split):
     """Two-stream (and graph-replayed) pair encode == the single-tower calls, bit for bit;
     a replayed graph sees new input contents behind the same pointers."""
     m, cfg, sd, lora = _model("tiny", "float16", max_batch=16)
@@ -164,11 +165,11 @@ def test_encode_pair_matches_separate(graph):
     oi = torch.empty_like(a_i)
     ot = torch.empty_like(a_t)
     for _ in range(3):
-        m.encode_pair(imgs, ids, out_img=oi, out_txt=ot, graph=graph)
+        m.encode_pair(imgs, ids, out_img=oi, out_txt=ot, graph=graph, split=split)
         torch.cuda.synchronize()
         assert torch.equal(oi, a_i) and torch.equal(ot, a_t)
     imgs.copy_(torch.from_numpy(syn.images_u8(7, cfg.image_size, 41)).cuda())
-    m.encode_pair(imgs, ids, out_img=oi, out_txt=ot, graph=graph)
+    m.encode_pair(imgs, ids, out_img=oi, out_txt=ot, graph=graph, split=split)
     assert torch.equal(oi, m.encode_pixels(imgs))
     with pytest.raises(ValueError):
         m.encode_pair(imgs.cpu(), ids)

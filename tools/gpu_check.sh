@@ -16,6 +16,11 @@ for st in $STAGES; do
     bench)
       timeout -k 10 900 python bench.py ${BENCH_ARGS:-} > gpurun_out/bench.json 2> gpurun_out/bench.err
       rc=$?; echo "bench rc=$rc"; cat gpurun_out/bench.json; tail -5 gpurun_out/bench.err; [ $rc -eq 0 ] || exit $rc ;;
+    splits)
+      for sp in 1 2 3 4; do
+        timeout -k 10 300 python bench.py --no-search --no-cpu-baseline --split $sp > gpurun_out/bench_split$sp.json 2> gpurun_out/bench_split$sp.err
+        rc=$?; echo "split $sp rc=$rc"; cat gpurun_out/bench_split$sp.json; [ $rc -eq 0 ] || exit $rc
+      done ;;
     sweep)
       timeout -k 10 600 python tools/gemm_sweep.py > gpurun_out/sweep.jsonl 2> gpurun_out/sweep.err
       rc=$?; echo "sweep rc=$rc"; cat gpurun_out/sweep.jsonl | head -80; tail -3 gpurun_out/sweep.err; [ $rc -eq 0 ] || exit $rc ;;
