@@ -8,6 +8,20 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+
+// Raw buffer descriptor over [base, base + 2 GiB) built from wave-uniform inputs (made
+// provable with readfirstlane, so hipcc emits no waterfall loop). A lane passing
+// BUF_OOB as its byte offset has its store dropped / its load return 0 by the hardware
+// range check: predication without branches (a branch per store makes the waitcnt pass
+// fall back to vmcnt(0) in front of every store).
+constexpr uint32_t BUF_OOB = 0x80000000u;
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void* base) {
+  const uint64_t b = (uint64_t)base;
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)b);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(b >> 32));
+  return __builtin_amdgcn_make_buffer_rsrc((void*)(((uint64_t)hi << 32) | lo), 0, 0x7FFFFFF0, 0x00020000);
+}
 
 namespace clm {
 

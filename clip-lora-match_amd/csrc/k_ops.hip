@@ -255,6 +255,11 @@ __global__ __launch_bounds__(256) void pool_project_kernel(const float* h, int64
                                                            const int32_t* ids, int eos, const float* g,
                                                            const float* bt, float eps, const float* projT, int D,
                                                            float* tmp) {
+  // Batch invariance: a row's arithmetic must not depend on its slot r in the PRB group.
+  // With implicit contraction the compiler fuses (or SLP-packs unfused) the unrolled
+  // per-slot chains differently, 1-ulp apart; so no implicit contraction here, and every
+  // intended FMA is an explicit fmaf.
+#pragma clang fp contract(off)
   extern __shared__ __attribute__((aligned(16))) float sm[];
   float* y = sm;                   // [d][PRB]
   float* part_sum = sm + d * PRB;  // [4][PRB][64]
@@ -290,9 +295,9 @@ __global__ __launch_bounds__(256) void pool_project_kernel(const float* h, int64
     for (int e = lane; e < d; e += 64) s += x[e];
     const float mean = wave_sum(s) / d;
     float v = 0.f;
-    for (int e = lane; e < d; e += 64) { const float t = x[e] - mean; v += t * t; }
+    for (int e = lane; e < d; e += 64) { const float t = x[e] - mean; v = fmaf(t, t, v); }
     const float rstd = 1.0f / sqrtf(wave_sum(v) / d + eps);
-    for (int e = lane; e < d; e += 64) y[e * PRB + rr] = (x[e] - mean) * rstd * g[e] + bt[e];
+    for (int e = lane; e < d; e += 64) y[e * PRB + rr] = fmaf((x[e] - mean) * rstd, g[e], bt[e]);
   }
   __syncthreads();
   const int c = lane, part = wid;
@@ -306,8 +311,10 @@ __global__ __launch_bounds__(256) void pool_project_kernel(const float* h, int64
     for (int i = i0; i < i1; ++i) {
       const float w = projT[(int64_t)i * D + j];
       const float4 ya = *(const float4*)(y + i * PRB), yb = *(const float4*)(y + i * PRB + 4);
-      acc[0] += ya.x * w; acc[1] += ya.y * w; acc[2] += ya.z * w; acc[3] += ya.w * w;
-      acc[4] += yb.x * w; acc[5] += yb.y * w; acc[6] += yb.z * w; acc[7] += yb.w * w;
+      acc[0] = fmaf(ya.x, w, acc[0]); acc[1] = fmaf(ya.y, w, acc[1]);
+      acc[2] = fmaf(ya.z, w, acc[2]); acc[3] = fmaf(ya.w, w, acc[3]);
+      acc[4] = fmaf(yb.x, w, acc[4]); acc[5] = fmaf(yb.y, w, acc[5]);
+      acc[6] = fmaf(yb.z, w, acc[6]); acc[7] = fmaf(yb.w, w, acc[7]);
     }
   }
 #pragma unroll
@@ -327,12 +334,13 @@ __global__ __launch_bounds__(256) void pool_project_kernel(const float* h, int64
 // out[b] = tmp[b] / ||tmp[b]||_2 (models/clip_model.py:116,148) or a plain copy; f32 or f16 out
 __global__ __launch_bounds__(256) void finish_rows_kernel(const float* tmp, int B, int D, void* out, int out_dtype,
                                                           int normalize) {
+#pragma clang fp contract(off)
   const int lane = threadIdx.x & 63;
   const int b = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (b >= B) return;
   const float* r = tmp + (int64_t)b * D;
   float s = 0.f;
-  for (int e = lane; e < D; e += 64) s += r[e] * r[e];
+  for (int e = lane; e < D; e += 64) s = fmaf(r[e], r[e], s);
   const float nrm = normalize ? sqrtf(wave_sum(s)) : 1.f;
   for (int e = lane; e < D; e += 64) {
     const float o = normalize ? r[e] / nrm : r[e];

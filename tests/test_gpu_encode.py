@@ -152,6 +152,19 @@ def test_bad_inputs_raise():
         m.encode_ids(torch.full((1, 4), cfg.vocab + 5, dtype=torch.int32))
 
 
+@pytest.mark.parametrize("dtype", ["float16", "bfloat16"])
+def test_batch_invariance(dtype):
+    """An item's embedding does not depend on the batch it was encoded in (bit for bit):
+    what lets encode_pair cut a batch into concurrent sub-batches."""
+    m, cfg, sd, lora = _model("tiny", dtype, max_batch=16)
+    imgs = torch.from_numpy(syn.images_u8(7, cfg.image_size, 51)).cuda()
+    ids = torch.from_numpy(syn.captions(7, cfg.max_pos, cfg.bos_token_id, cfg.eos_token_id, 52)).cuda()
+    fi, ft = m.encode_pixels(imgs), m.encode_ids(ids)
+    for a, b in ((0, 3), (3, 7), (2, 3)):
+        assert torch.equal(m.encode_pixels(imgs[a:b]), fi[a:b]), ("image", a, b)
+        assert torch.equal(m.encode_ids(ids[a:b]), ft[a:b]), ("text", a, b)
+
+
 @pytest.mark.parametrize("graph", [False, True])
 @pytest.mark.parametrize("split", [1, 2, 3])
 def test_encode_pair_matches_separate(graph, split):

@@ -50,6 +50,36 @@ def test_gemm_epilogues_vs_torch(dtype, cfg, shape):
     assert (sc - refs).abs().max() <= 1e-4 * refs.abs().max() + 1e-6
 
 
+@pytest.mark.parametrize("epi", ["STORE", "GELU", "RESID", "SCORE"])
+@pytest.mark.parametrize("N", [192, 200])
+def test_gemm_row_invariance_and_bounds(epi, N):
+    """Every tile config gives bit-identical rows (same K order), a row's value does not
+    depend on M or on which rows share its tile (sub-batches == full batch), and nothing
+    outside [M, N) of the output is written (padding columns of ldo > N, rows >= M)."""
+    dtype, M, K, ldo, split = "float16", 119, 256, N + 24, 51
+    code = getattr(C, f"CLM_EPI_{epi}")
+    g = torch.Generator(device="cuda").manual_seed(N)
+    A = torch.randn((M, K), generator=g, device="cuda").half()
+    W = (torch.randn((N, K), generator=g, device="cuda") / K ** 0.5).half()
+    bias = torch.randn(N, generator=g, device="cuda") if epi != "SCORE" else None
+    rs = torch.rand(M, generator=g, device="cuda") + 0.5 if epi == "SCORE" else None
+    cs = torch.rand(N, generator=g, device="cuda") + 0.5 if epi == "SCORE" else None
+    odt = torch.float32 if epi in ("RESID", "SCORE") else torch.float16
+    init = torch.randn((M + 40, ldo), generator=g, device="cuda").to(odt)
+    ref = None
+    for cfg in list(range(C.lib().clm_gemm_num_configs())) + [-1]:
+        out = init.clone()
+        _gemm(dtype, code, cfg, A, W, out[:M], bias, rs, cs)
+        assert torch.equal(out[:, N:], init[:, N:]) and torch.equal(out[M:], init[M:]), f"cfg {cfg} wrote outside"
+        parts = init.clone()   # two sub-batches of rows [0, split) and [split, M)
+        _gemm(dtype, code, cfg, A[:split], W, parts[:split], bias, rs[:split] if rs is not None else None, cs)
+        _gemm(dtype, code, cfg, A[split:], W, parts[split:M], bias, rs[split:] if rs is not None else None, cs)
+        assert torch.equal(parts, out), f"cfg {cfg}: sub-batch rows differ from the full batch"
+        if ref is None:
+            ref = out
+        assert torch.equal(out, ref), f"cfg {cfg} differs from cfg 0"
+
+
 def test_gemm_asymmetric_identity():
     """A = I catches a transposed C write (cdna_hip_programming §3 'A=I-check with ASYMMETRIC B')."""
     n = 128
