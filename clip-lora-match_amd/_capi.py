@@ -89,6 +89,7 @@ def lib():
         "clm_gemm": (c_int, [c_int, c_int, c_int, c_int, c_void_p, c_int64, c_void_p, c_int64, c_int, c_int, c_int,
                              c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_void_p]),
         "clm_gemm_num_configs": (c_int, []),
+        "clm_debug_set": (None, [c_int]),
         "clm_attention": (c_int, [c_int, c_int, c_int, c_void_p, c_void_p, c_int64, c_int, c_int, c_int, c_void_p]),
         "clm_prof_read": (c_int, [c_void_p, c_int, POINTER(ctypes.c_double), POINTER(ctypes.c_double),
                                   POINTER(c_int64)]),
@@ -107,7 +108,7 @@ EXPORTED = (
     "clm_index_size", "clm_index_reset", "clm_index_set_offset", "clm_index_read", "clm_index_search", "clm_index_stats",
     "clm_cosine_scores", "clm_topk_merge", "clm_l2_normalize", "clm_last_error", "clm_version",
     "clm_model_desc_size", "clm_prof_enable", "clm_prof_read", "clm_gemm", "clm_gemm_num_configs",
-    "clm_attention",
+    "clm_attention", "clm_debug_set",
 )
 CLM_EPI_STORE, CLM_EPI_GELU, CLM_EPI_RESID, CLM_EPI_SCORE = 0, 1, 2, 4
 CLM_PROF_GEMM, CLM_PROF_ATTN, CLM_PROF_LN, CLM_PROF_OTHER = 0, 1, 2, 3

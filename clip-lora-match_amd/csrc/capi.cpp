@@ -31,6 +31,8 @@ using namespace clm;
 namespace {
 
 thread_local std::string g_err;
+// clm_debug_set / $CLM_GEMM_DEBUG: GemmArgs::debug of clm_gemm (micro-benchmarks only)
+int g_gemm_debug = getenv("CLM_GEMM_DEBUG") ? atoi(getenv("CLM_GEMM_DEBUG")) : 0;
 int fail(int code, const std::string& msg) {
   g_err = msg;
   return code;
@@ -601,14 +603,15 @@ int clm_gemm(int hip_device, int dtype, int epilogue, int config, const void* A,
   GemmArgs a{};
   a.A = (const u16*)A; a.lda = lda; a.W = (const u16*)W; a.ldw = ldw; a.M = M; a.N = N; a.K = K;
   a.out = out; a.ldo = ldo; a.bias = bias; a.rscale = rscale; a.cscale = cscale;
-  static const int dbg = getenv("CLM_GEMM_DEBUG") ? atoi(getenv("CLM_GEMM_DEBUG")) : 0;
-  a.debug = dbg;
+  a.debug = g_gemm_debug;
   hipError_t e = gemm_cfg(dtype == CLM_BF16, epilogue, config, a, (hipStream_t)stream);
   if (e != hipSuccess) return fail(CLM_E_HIP, std::string("gemm: ") + hipGetErrorString(e));
   return CLM_OK;
 }
 
 int clm_gemm_num_configs(void) { return gemm_num_configs(); }
+
+void clm_debug_set(int flags) { g_gemm_debug = flags; }
 
 int clm_attention(int hip_device, int dtype, int causal, const void* qkv, void* out, int64_t ldo, int B, int T,
                   int H, void* stream) {

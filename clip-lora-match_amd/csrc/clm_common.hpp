@@ -16,11 +16,11 @@ typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 // range check: predication without branches (a branch per store makes the waitcnt pass
 // fall back to vmcnt(0) in front of every store).
 constexpr uint32_t BUF_OOB = 0x80000000u;
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void* base) {
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void* base, int num_records = 0x7FFFFFF0) {
   const uint64_t b = (uint64_t)base;
   const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)b);
   const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(b >> 32));
-  return __builtin_amdgcn_make_buffer_rsrc((void*)(((uint64_t)hi << 32) | lo), 0, 0x7FFFFFF0, 0x00020000);
+  return __builtin_amdgcn_make_buffer_rsrc((void*)(((uint64_t)hi << 32) | lo), 0, num_records, 0x00020000);
 }
 
 namespace clm {
@@ -76,8 +76,12 @@ __device__ __forceinline__ float group16_max(float v) {
 }
 
 __device__ __forceinline__ float quick_gelu(float x) {
-  // TF/activations.py:123  x * sigmoid(1.702 x)
-  return x / (1.0f + __expf(-1.702f * x));
+  // TF/activations.py:123  x * sigmoid(1.702 x), as x * rcp(1 + 2^(-1.702 log2(e) x)):
+  // v_exp_f32 + v_rcp_f32 (1 ulp) instead of an IEEE division (4 v_div_* + v_fma per value,
+  // which made the fc1 epilogue cost as much as a third of its main loop). Limits stay exact:
+  // x -> -inf gives 2^+big = inf, rcp = 0, -0; x -> +inf gives x.
+  const float t = __builtin_amdgcn_exp2f(-2.4554669595930157f * x);
+  return x * __builtin_amdgcn_rcpf(1.0f + t);
 }
 
 // XOR swizzle of 16-byte chunks inside 128-byte LDS rows: conflict-free

@@ -20,6 +20,7 @@
 //    (8 B bf16 / 16 B fp32) instead of 2-byte scatter;
 //  * workgroup ids are remapped XCD-aware so the N-tiles sharing one A row-panel
 //    (and its L2 lines) run on one XCD.
+#include <algorithm>
 #include <cstdlib>
 
 #include "kernels.hpp"
@@ -40,20 +41,18 @@ struct Cfg {
   static constexpr int LA = BM / 8 / NW;   // A DMA pieces (8 rows) per wave per K-tile
   static constexpr int LB = BN / 8 / NW;
   static constexpr int L = LA + LB;        // vmcnt units per K-tile
+  // workgroups per CU the LDS ring allows, and the waves per SIMD that makes: given to
+  // __launch_bounds__ so the register allocation does not cost that occupancy
+  static constexpr int WG_PER_CU = (160 * 1024) / LDS;
+  static constexpr int WAVES_PER_EU = WG_PER_CU * NW / 4 < 1 ? 1 : (WG_PER_CU * NW / 4 > 8 ? 8 : WG_PER_CU * NW / 4);
   static_assert(BM % (8 * NW) == 0 && BN % (8 * NW) == 0, "rows must split evenly over waves");
   static_assert(TM >= 1 && TN >= 1, "wave tile too small");
 };
 
 template <int N>
 __device__ __forceinline__ void wait_vmcnt() {
-  if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  else if constexpr (N == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-  else if constexpr (N == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-  else if constexpr (N == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-  else if constexpr (N == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-  else if constexpr (N == 12) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
-  else if constexpr (N == 16) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
-  else static_assert(N < 0, "unsupported vmcnt");
+  static_assert(N >= 0 && N <= 63, "vmcnt is a 6-bit counter");
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
 __device__ __forceinline__ void lds_barrier() {
@@ -105,111 +104,19 @@ __device__ __forceinline__ void epilogue_scalar(const GemmArgs& g, const f32x4 (
   }
 }
 
+// Epilogue of one BM x BN tile from the accumulators.
 template <bool BF, int EPI, int BM, int BN, int WM, int WN, int STAGES>
-__global__ __launch_bounds__(WM * WN * 64) void gemm_kernel(GemmArgs g) {
+__device__ __forceinline__ void epilogue(const GemmArgs& g, const f32x4 (&acc)[BM / WM / 16][BN / WN / 16], int m0,
+                                         int n0, int wm, int wn, int lane) {
   using C = Cfg<BM, BN, WM, WN, STAGES>;
-  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int ntn = (g.N + BN - 1) / BN, ntm = (g.M + BM - 1) / BM;
-  const int t = xcd_remap(blockIdx.x, ntn * ntm);
-  int tm, tn;
-  if (g.m_fastest) {          // every query tile of one index tile back to back (search)
-    tm = t % ntm;
-    tn = t / ntm;
-  } else {                    // grouped raster: GM row-panels x all N-tiles per group, M inner,
-    constexpr int GM = 8;     // so an XCD's concurrent tiles share A panels and W tiles in L2
-    const int group = t / (GM * ntn);
-    const int first_m = group * GM;
-    const int gsz = min(GM, ntm - first_m);
-    const int r = t - group * GM * ntn;
-    tm = first_m + r % gsz;
-    tn = r / gsz;
-  }
-  const int m0 = tm * BM, n0 = tn * BN;
-
-  // per-lane DMA sources: piece i of this wave covers tile rows (wid*LA + i)*8 .. +8
-  const int r8 = lane >> 3, pc = lane & 7;
-  const u16* a_src[C::LA];
-  const u16* w_src[C::LB];
-#pragma unroll
-  for (int i = 0; i < C::LA; ++i) {
-    const int row = (wid * C::LA + i) * 8 + r8;
-    a_src[i] = g.A + (int64_t)min(m0 + row, g.M - 1) * g.lda + (pc ^ ((row >> 1) & 7)) * 8;
-  }
-#pragma unroll
-  for (int i = 0; i < C::LB; ++i) {
-    const int row = (wid * C::LB + i) * 8 + r8;
-    w_src[i] = g.W + (int64_t)min(n0 + row, g.N - 1) * g.ldw + (pc ^ ((row >> 1) & 7)) * 8;
-  }
-  auto stage = [&](int kt, int s) {
-    uint8_t* base = smem + s * C::STAGE_BYTES;
-#pragma unroll
-    for (int i = 0; i < C::LA; ++i)
-      __builtin_amdgcn_global_load_lds((const void*)(a_src[i] + kt * BK),
-                                       (void*)(base + (wid * C::LA + i) * 1024), 16, 0, 0);
-#pragma unroll
-    for (int i = 0; i < C::LB; ++i)
-      __builtin_amdgcn_global_load_lds((const void*)(w_src[i] + kt * BK),
-                                       (void*)(base + BM * 128 + (wid * C::LB + i) * 1024), 16, 0, 0);
-  };
-
-  const int wm = wid / WN, wn = wid % WN;
-  f32x4 acc[C::TM][C::TN];
-#pragma unroll
-  for (int i = 0; i < C::TM; ++i)
-#pragma unroll
-    for (int j = 0; j < C::TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  const int nk = g.K / BK;
-#pragma unroll
-  for (int s = 0; s < STAGES - 1; ++s)
-    if (s < nk) stage(s, s);
-
-  for (int kt = 0; kt < nk; ++kt) {
-    // retire tile kt's DMA (leave the younger tiles in flight), then one barrier makes
-    // it visible to every wave and proves tile kt-1's buffer is no longer being read
-    if (kt + STAGES - 2 < nk) wait_vmcnt<C::L * (STAGES - 2)>();
-    else wait_vmcnt<0>();
-    lds_barrier();
-    if (kt + STAGES - 1 < nk) stage(kt + STAGES - 1, (kt + STAGES - 1) % STAGES);
-    const uint8_t* sa = smem + (kt % STAGES) * C::STAGE_BYTES;
-    const uint8_t* sb = sa + BM * 128;
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
-      const int c = kk * 4 + (lane >> 4);
-      u32x4 af[C::TM], bw[C::TN];
-#pragma unroll
-      for (int mb = 0; mb < C::TM; ++mb) {
-        const int row = wm * (BM / WM) + mb * 16 + (lane & 15);
-        af[mb] = *(const u32x4*)(sa + row * 128 + swz(row, c) * 16);
-      }
-#pragma unroll
-      for (int nb = 0; nb < C::TN; ++nb) {
-        const int row = wn * (BN / WN) + nb * 16 + (lane & 15);
-        bw[nb] = *(const u32x4*)(sb + row * 128 + swz(row, c) * 16);
-      }
-#pragma unroll
-      for (int mb = 0; mb < C::TM; ++mb)
-#pragma unroll
-        for (int nb = 0; nb < C::TN; ++nb) acc[mb][nb] = mfma16<BF>(bw[nb], af[mb], acc[mb][nb]);
-    }
-  }
-
-  if (g.debug & 1) {   // timing diagnostic: main loop only
-#pragma unroll
-    for (int mb = 0; mb < C::TM; ++mb)
-#pragma unroll
-      for (int nb = 0; nb < C::TN; ++nb) asm volatile("" ::"v"(acc[mb][nb]));
-    return;
-  }
-  // ---- epilogue: lane owns C[m, n..n+3], m = wrow + 16*mb, n = wcol + 16*nb.
+  // lane owns C[m, n..n+3], m = wrow + 16*mb, n = wcol + 16*nb.
   // Every global load of the epilogue (bias / cscale / row scales, residual, pos rows) is
   // issued in a batch BEFORE the stores it feeds: vmcnt counts loads and stores together in
   // issue order, so a load placed after a store waits for that store's round trip, and a
   // per-block load -> store sequence costs one full memory latency per 16x16 block.
   // (An LDS-staged full-row variant measured slower on every encoder shape:
   // profiles/r01_v5_gemm_split_staged_epilogue.jsonl.)
+  const int nrec = (g.debug & 2) ? 0 : 0x7FFFFFF0;   // diagnostic: drop every epilogue store
   const int wrow = m0 + wm * (BM / WM) + (lane & 15);
   const int wcol = n0 + wn * (BN / WN) + (lane >> 4) * 4;
   if ((g.N % 4) != 0 || (g.ldo % 4) != 0) {   // ragged N: scalar tail path
@@ -240,7 +147,7 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_kernel(GemmArgs g) {
       }
       return u32x2{pack2<BF>(v[0], v[1]), pack2<BF>(v[2], v[3])};
     };
-    const auto ob = buf_rsrc((const u16*)g.out + (int64_t)m0 * g.ldo);   // tile-relative offsets
+    const auto ob = buf_rsrc((const u16*)g.out + (int64_t)m0 * g.ldo, nrec);   // tile-relative offsets
     const bool wide = (C::TN % 2) == 0 && (g.N % 8) == 0 && (g.ldo % 8) == 0 && ((uintptr_t)g.out & 15) == 0;
     if (wide) {
       // 16-B stores: v_permlane16_swap trades the odd 16-lane groups' block-nb words with the
@@ -280,7 +187,7 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_kernel(GemmArgs g) {
     // No branches: out-of-range lanes use BUF_OOB.
     // Patch rows skip each image's class row: out row = m + m / group + 1 (vision embeddings).
     const int64_t orow0 = EPI == EPI_PATCH ? (int64_t)m0 + m0 / g.group + 1 : m0;
-    const auto ob = buf_rsrc((const float*)g.out + orow0 * g.ldo);
+    const auto ob = buf_rsrc((const float*)g.out + orow0 * g.ldo, nrec);
     const auto ab = buf_rsrc(EPI == EPI_PATCH ? (const void*)g.aux : g.out);   // pos rows (PATCH)
     auto offs = [&](int mb, int nb, uint32_t& oo, uint32_t& ao) {
       const int m = wrow + mb * 16, n = wcol + nb * 16;
@@ -346,7 +253,7 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_kernel(GemmArgs g) {
       if constexpr (EPI == EPI_FILTER) th[mb] = m < g.M ? g.theta[(int64_t)m * g.theta_ld] : 0.f;
     }
     if constexpr (EPI == EPI_SCORE) {
-      const auto ob = buf_rsrc((const float*)g.out + (int64_t)m0 * g.ldo);
+      const auto ob = buf_rsrc((const float*)g.out + (int64_t)m0 * g.ldo, nrec);
 #pragma unroll
       for (int mb = 0; mb < C::TM; ++mb) {
         const int m = wrow + mb * 16;
@@ -389,6 +296,160 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_kernel(GemmArgs g) {
   }
 }
 
+// Stores (vector-memory instructions) one tile's epilogue issues per wave at least, on the
+// vector paths; the main loop's counted vmcnt leaves this many in flight after a tile end
+// (a smaller count than actually issued only over-waits). FILTER stores in branches: 0.
+template <int EPI, int TM, int TN>
+constexpr int epi_min_stores() {
+  return (EPI == EPI_STORE || EPI == EPI_GELU) ? TM * TN / 2 : EPI == EPI_FILTER ? 0 : TM * TN;
+}
+
+// Persistent: workgroup b takes tiles xb, xb + G, xb + 2G, ... (G = gridDim.x <= tiles,
+// xb = XCD-aware remap of b), and its LDS-DMA ring runs ACROSS tile boundaries: the first
+// K-tiles of tile i+1 are issued before tile i's epilogue, so they land while the epilogue
+// runs, and the epilogue's stores drain under tile i+1's main loop (counted vmcnt that
+// leaves them in flight). A one-tile-per-workgroup grid is the plain non-persistent GEMM.
+template <bool BF, int EPI, int BM, int BN, int WM, int WN, int STAGES>
+__global__ __launch_bounds__(WM * WN * 64, (Cfg<BM, BN, WM, WN, STAGES>::WAVES_PER_EU)) void gemm_kernel(GemmArgs g) {
+  using C = Cfg<BM, BN, WM, WN, STAGES>;
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int ntn = (g.N + BN - 1) / BN, ntm = (g.M + BM - 1) / BM;
+  const int ntiles = ntn * ntm, G = gridDim.x;
+  const int xb = xcd_remap(blockIdx.x, G);
+  const int n_my = (ntiles - 1 - xb) / G + 1;
+  const int nk = g.K / BK;
+  const int S = n_my * nk;   // K-steps of all this workgroup's tiles, one ring
+
+  auto coords = [&](int i, int& m0, int& n0) {
+    const int t = i * G + xb;
+    int tm, tn;
+    if (g.m_fastest) {          // every query tile of one index tile back to back (search)
+      tm = t % ntm;
+      tn = t / ntm;
+    } else {                    // grouped raster: GM row-panels x all N-tiles per group, M inner,
+      constexpr int GM = 8;     // so an XCD's concurrent tiles share A panels and W tiles in L2
+      const int group = t / (GM * ntn);
+      const int first_m = group * GM;
+      const int gsz = min(GM, ntm - first_m);
+      const int r = t - group * GM * ntn;
+      tm = first_m + r % gsz;
+      tn = r / gsz;
+    }
+    m0 = tm * BM;
+    n0 = tn * BN;
+  };
+
+  // loader state: per-lane DMA sources of the tile being loaded (piece j of this wave covers
+  // tile rows (wid*LA + j)*8 .. +8), re-pointed when the ring crosses into the next tile
+  const int r8 = lane >> 3, pc = lane & 7;
+  const u16* a_src[C::LA];
+  const u16* w_src[C::LB];
+  auto point = [&](int i) {
+    int m0, n0;
+    coords(i, m0, n0);
+#pragma unroll
+    for (int j = 0; j < C::LA; ++j) {
+      const int row = (wid * C::LA + j) * 8 + r8;
+      a_src[j] = g.A + (int64_t)min(m0 + row, g.M - 1) * g.lda + (pc ^ ((row >> 1) & 7)) * 8;
+    }
+#pragma unroll
+    for (int j = 0; j < C::LB; ++j) {
+      const int row = (wid * C::LB + j) * 8 + r8;
+      w_src[j] = g.W + (int64_t)min(n0 + row, g.N - 1) * g.ldw + (pc ^ ((row >> 1) & 7)) * 8;
+    }
+  };
+  int ld_i = 0, ld_kt = 0;
+  point(0);
+  auto stage_next = [&](int buf) {   // DMA of the ring's next K-step into LDS buffer buf
+    uint8_t* base = smem + buf * C::STAGE_BYTES;
+#pragma unroll
+    for (int j = 0; j < C::LA; ++j)
+      __builtin_amdgcn_global_load_lds((const void*)(a_src[j] + ld_kt * BK),
+                                       (void*)(base + (wid * C::LA + j) * 1024), 16, 0, 0);
+#pragma unroll
+    for (int j = 0; j < C::LB; ++j)
+      __builtin_amdgcn_global_load_lds((const void*)(w_src[j] + ld_kt * BK),
+                                       (void*)(base + BM * 128 + (wid * C::LB + j) * 1024), 16, 0, 0);
+    if (++ld_kt == nk) {
+      ld_kt = 0;
+      if (++ld_i < n_my) point(ld_i);
+    }
+  };
+
+  const int wm = wid / WN, wn = wid % WN;
+  f32x4 acc[C::TM][C::TN];
+#pragma unroll
+  for (int i = 0; i < C::TM; ++i)
+#pragma unroll
+    for (int j = 0; j < C::TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+#pragma unroll
+  for (int s = 0; s < STAGES - 1; ++s)
+    if (s < S) stage_next(s);
+
+  // stores a tile end leaves in flight (the ragged scalar path stores in branches: none counted)
+  constexpr int E = epi_min_stores<EPI, C::TM, C::TN>();
+  const bool vec_epi = (g.N % 4) == 0 && (g.ldo % 4) == 0 && !(g.debug & 1);
+  int c_i = 0, c_kt = 0, m0, n0;
+  coords(0, m0, n0);
+  bool prev_end = false;
+  for (int s = 0; s < S; ++s) {
+    // retire K-step s's DMA, leaving younger ones in flight: the STAGES-2 later K-steps' DMA
+    // and, right after a tile end, that epilogue's stores (issued after this DMA)
+    const bool more = s + STAGES - 2 < S;
+    const bool pe = prev_end && vec_epi;
+    if (more) {
+      if (pe) wait_vmcnt<C::L * (STAGES - 2) + E>();
+      else wait_vmcnt<C::L * (STAGES - 2)>();
+    } else {
+      if (pe) wait_vmcnt<E>();
+      else wait_vmcnt<0>();
+    }
+    lds_barrier();
+    if (s + STAGES - 1 < S) stage_next((s + STAGES - 1) % STAGES);
+    const uint8_t* sa = smem + (s % STAGES) * C::STAGE_BYTES;
+    const uint8_t* sb = sa + BM * 128;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const int c = kk * 4 + (lane >> 4);
+      u32x4 af[C::TM], bw[C::TN];
+#pragma unroll
+      for (int mb = 0; mb < C::TM; ++mb) {
+        const int row = wm * (BM / WM) + mb * 16 + (lane & 15);
+        af[mb] = *(const u32x4*)(sa + row * 128 + swz(row, c) * 16);
+      }
+#pragma unroll
+      for (int nb = 0; nb < C::TN; ++nb) {
+        const int row = wn * (BN / WN) + nb * 16 + (lane & 15);
+        bw[nb] = *(const u32x4*)(sb + row * 128 + swz(row, c) * 16);
+      }
+#pragma unroll
+      for (int mb = 0; mb < C::TM; ++mb)
+#pragma unroll
+        for (int nb = 0; nb < C::TN; ++nb) acc[mb][nb] = mfma16<BF>(bw[nb], af[mb], acc[mb][nb]);
+    }
+    prev_end = ++c_kt == nk;
+    if (prev_end) {
+      if (g.debug & 1) {   // timing diagnostic: main loop only
+#pragma unroll
+        for (int mb = 0; mb < C::TM; ++mb)
+#pragma unroll
+          for (int nb = 0; nb < C::TN; ++nb) asm volatile("" ::"v"(acc[mb][nb]));
+      } else {
+        epilogue<BF, EPI, BM, BN, WM, WN, STAGES>(g, acc, m0, n0, wm, wn, lane);
+      }
+#pragma unroll
+      for (int i = 0; i < C::TM; ++i)
+#pragma unroll
+        for (int j = 0; j < C::TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      c_kt = 0;
+      if (++c_i < n_my) coords(c_i, m0, n0);
+    }
+  }
+}
+
 template <bool BF, int EPI, int BM, int BN, int WM, int WN, int STAGES>
 hipError_t launch_cfg(const GemmArgs& g, hipStream_t s) {
   using C = Cfg<BM, BN, WM, WN, STAGES>;
@@ -401,7 +462,18 @@ hipError_t launch_cfg(const GemmArgs& g, hipStream_t s) {
     if (e != hipSuccess) return e;
     __atomic_fetch_or(&dev_done, 1u << (dev & 31), __ATOMIC_RELEASE);
   }
-  const int nwg = ((g.N + BN - 1) / BN) * ((g.M + BM - 1) / BM);
+  // persistent grid: at most one workgroup per resident slot (occupancy x CUs, per device)
+  static int slots[32] = {};
+  int& sl = slots[dev & 31];
+  if (sl == 0) {
+    int per_cu = 0, cus = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, C::NT, C::LDS) != hipSuccess || per_cu < 1) per_cu = 1;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1) cus = 256;
+    (void)hipGetLastError();
+    sl = per_cu * cus;
+  }
+  const int tiles = ((g.N + BN - 1) / BN) * ((g.M + BM - 1) / BM);
+  const int nwg = (g.debug & 4) ? tiles : std::min(tiles, sl);   // debug bit 2: one tile per workgroup
   kern<<<dim3(nwg), dim3(C::NT), C::LDS, s>>>(g);
   return hipGetLastError();
 }

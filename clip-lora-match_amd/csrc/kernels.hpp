@@ -28,7 +28,8 @@ struct GemmArgs {
   // EPI_FILTER
   const float* theta; int64_t theta_ld; int* cnt; float* cand_s; int64_t* cand_i; int cap; int64_t base;
   int m_fastest;   // tile order: 1 = consecutive workgroups walk M (share one W tile)
-  int debug;       // diagnostic builds only: 1 = skip the epilogue (accumulators kept live)
+  int debug;       // diagnostics only: 1 = skip the epilogue (accumulators kept live), 2 = drop its
+                   // stores, 4 = one tile per workgroup (non-persistent grid)
 };
 
 hipError_t gemm(bool bf16, int epi, const GemmArgs& g, hipStream_t s);

@@ -163,6 +163,10 @@ int clm_gemm(int hip_device, int dtype, int epilogue, int config, const void* A,
              const void* W, int64_t ldw, int M, int N, int K, void* out, int64_t ldo,
              const float* bias, const float* rscale, const float* cscale, void* stream);
 int clm_gemm_num_configs(void);
+/* diagnostic flags for later clm_gemm calls (micro-benchmarks only; 0 in production):
+ * bit 0 = skip the epilogue (accumulators kept live), bit 1 = run the epilogue but drop
+ * every store. Initialised from $CLM_GEMM_DEBUG. */
+void clm_debug_set(int flags);
 /* attention over qkv [B*T, 3*H*64] (q pre-scaled), out [B*T, ldo] (device pointers) */
 int clm_attention(int hip_device, int dtype, int causal, const void* qkv, void* out, int64_t ldo,
                   int B, int T, int H, void* stream);

@@ -80,6 +80,35 @@ def test_gemm_row_invariance_and_bounds(epi, N):
         assert torch.equal(out, ref), f"cfg {cfg} differs from cfg 0"
 
 
+@pytest.mark.parametrize("shape", [(8200, 2100, 64), (8200, 2100, 192), (8200, 2098, 128)])
+def test_gemm_persistent_multi_tile(shape):
+    """Grids with more tiles than resident workgroups: each workgroup walks several tiles with
+    one LDS-DMA ring across tile boundaries (K = 64: every K-step ends a tile; N = 2098: the
+    ragged scalar epilogue). Must equal the one-tile-per-workgroup grid bit for bit (debug
+    flag 4) and the fp32 reference."""
+    M, N, K = shape
+    g = torch.Generator(device="cuda").manual_seed(K)
+    A = torch.randn((M, K), generator=g, device="cuda").half()
+    W = (torch.randn((N, K), generator=g, device="cuda") / K ** 0.5).half()
+    bias = torch.randn(N, generator=g, device="cuda")
+    ref = A.float() @ W.float().T + bias
+    h0 = torch.randn((M, N), generator=g, device="cuda")
+    try:
+        for cfg in list(range(C.lib().clm_gemm_num_configs())) + [-1]:
+            for epi in (C.CLM_EPI_STORE, C.CLM_EPI_RESID):
+                outs = []
+                for dbg in (0, 4):
+                    C.lib().clm_debug_set(dbg)
+                    out = h0.clone() if epi == C.CLM_EPI_RESID else torch.empty((M, N), dtype=torch.half, device="cuda")
+                    _gemm("float16", epi, cfg, A, W, out, bias)
+                    outs.append(out)
+                assert torch.equal(outs[0], outs[1]), f"cfg {cfg} epi {epi}: persistent grid differs"
+                want = h0 + ref if epi == C.CLM_EPI_RESID else ref
+                assert (outs[0].float() - want).abs().max() <= 4e-3 * ref.abs().max(), f"cfg {cfg} epi {epi}"
+    finally:
+        C.lib().clm_debug_set(0)
+
+
 def test_gemm_asymmetric_identity():
     """A = I catches a transposed C write (cdna_hip_programming §3 'A=I-check with ASYMMETRIC B')."""
     n = 128
