@@ -21,7 +21,7 @@ def _gemm(dtype, epi, cfg, A, W, out, bias=None, rs=None, cs=None):
 
 
 @pytest.mark.parametrize("dtype", ["bfloat16", "float16"])
-@pytest.mark.parametrize("cfg", list(range(11)) + [-1])
+@pytest.mark.parametrize("cfg", list(range(19)) + [-1])
 @pytest.mark.parametrize("shape", [(333, 200, 128), (1000, 768, 768), (77, 2304, 512), (97, 100, 64), (65, 50, 128)])
 def test_gemm_epilogues_vs_torch(dtype, cfg, shape):
     M, N, K = shape
@@ -115,7 +115,7 @@ def test_gemm_asymmetric_identity():
     A = torch.eye(n, device="cuda", dtype=torch.float16)
     W = torch.arange(n * n, device="cuda", dtype=torch.float32).reshape(n, n).remainder(97).half()
     out = torch.empty((n, n), dtype=torch.float16, device="cuda")
-    for cfg in range(11):
+    for cfg in range(C.lib().clm_gemm_num_configs()):
         _gemm("float16", C.CLM_EPI_STORE, cfg, A, W, out)
         assert torch.equal(out, W.T.contiguous())
 
