@@ -9,6 +9,16 @@
 
 namespace clm {
 namespace gemm_detail {
+// percentage of the resident workgroup slots a persistent GEMM grid takes ($CLM_GEMM_GRID_PCT,
+// default 100): below 100 two GEMMs on different streams (image / text towers) can share the chip
+inline int grid_pct() {
+  static int pct = -1;
+  if (pct < 0) {
+    const char* e = getenv("CLM_GEMM_GRID_PCT");
+    pct = e ? std::max(1, std::min(100, atoi(e))) : 100;
+  }
+  return pct;
+}
 constexpr int BK = 64;
 
 template <int BM, int BN, int WM, int WN, int STAGES>

@@ -198,7 +198,7 @@ hipError_t launch_cfg(const GemmArgs& g, hipStream_t s) {
     sl = per_cu * cus;
   }
   const int tiles = ((g.N + BN - 1) / BN) * ((g.M + BM - 1) / BM);
-  const int nwg = (g.debug & 4) ? tiles : std::min(tiles, sl);   // debug bit 2: one tile per workgroup
+  const int nwg = (g.debug & 4) ? tiles : std::min(tiles, std::max(1, sl * grid_pct() / 100));   // debug bit 2: one tile per workgroup
   kern<<<dim3(nwg), dim3(C::NT), C::LDS, s>>>(g);
   return hipGetLastError();
 }

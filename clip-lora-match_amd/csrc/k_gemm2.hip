@@ -193,7 +193,7 @@ hipError_t launch_cfg2(const GemmArgs& g, hipStream_t s) {
     (void)hipGetLastError();
   }
   const int tiles = ((g.N + BN - 1) / BN) * ((g.M + BM - 1) / BM);
-  const int nwg = (g.debug & 4) ? tiles : std::min(tiles, cus);   // one workgroup per CU
+  const int nwg = (g.debug & 4) ? tiles : std::min(tiles, std::max(1, cus * grid_pct() / 100));   // <= one per CU
   kern<<<dim3(nwg), dim3(C::NT), C::LDS, s>>>(g);
   return hipGetLastError();
 }
