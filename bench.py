@@ -245,7 +245,8 @@ def main():
         "data": "synthetic (seeded uint8 224x224 RGB images, 77-token id captions; deterministic synthetic weights)",
         "config": {"workload": "ViT-B/32 + LoRA r=8 alpha=16 (q,k,v,out, both towers) encode + L2-normalise",
                    "execution": "sequential" if args.sequential else
-                       f"towers x sub-batches on streams (split={args.split or 'auto'}) + hipGraph replay",
+                       f"image / text towers concurrently on 2 HIP streams (sub-batches per tower: {args.split or 1})"
+                       " + hipGraph replay",
                    "per_gpu_batch": B, "global_batch": world * B, "seq_len": cfg.max_pos,
                    "image_size": cfg.image_size, "lora_mode": args.lora_mode,
                    "parallelism": f"dp{world}" + (" + all_gather(embeddings)" if world > 1 else "")},
