@@ -1137,7 +1137,11 @@ static int search_filtered(clm_index* x, const u16* q16, const float* qinv, int6
     x->samp_n = N;
     x->samp_S = S;
   }
-  const int64_t nqb = std::min<int64_t>(nq, std::max<int64_t>(256, ((int64_t)256 << 20) / ((int64_t)S * 4)));
+  // query block: its sample-score matrix (nqb x S fp32) is the workspace that bounds it; every
+  // block streams the whole index once through the filter GEMM, so fewer, larger blocks read
+  // the index fewer times (10 M x 512 fp16 = 10 GB per pass). $CLM_SEARCH_WS_MB overrides.
+  static const int64_t ws_mb = getenv("CLM_SEARCH_WS_MB") ? atoll(getenv("CLM_SEARCH_WS_MB")) : 8192;
+  const int64_t nqb = std::min<int64_t>(nq, std::max<int64_t>(256, (ws_mb << 20) / ((int64_t)S * 4)));
   size_t off = 0;
   auto take = [&](size_t bytes) { size_t o = off; off = round_up(off + bytes, 256); return o; };
   const size_t o_sc = take((size_t)nqb * S * 4);

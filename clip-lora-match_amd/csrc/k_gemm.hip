@@ -266,13 +266,13 @@ int pick_config(int epi, int M, int N) {
     const char* e = getenv("CLM_GEMM_CFG");
     forced = e ? atoi(e) : -1;
   }
-  if (forced >= 0 && forced < NCFG && !(epi == EPI_FILTER && forced >= 11)) return forced;
+  if (forced >= 0 && forced < NCFG) return forced;
   static int g2_epis = -1;   // epilogues served by G2 (bit per Epi); $CLM_G2_EPIS overrides
   if (g2_epis < 0) {
     const char* e = getenv("CLM_G2_EPIS");
     g2_epis = e ? atoi(e) : (1 << EPI_GELU);
   }
-  return (g2_epis >> epi) & 1 && epi != EPI_FILTER ? pick_from(MODELS_G2, M, N) : pick_from(MODELS, M, N);
+  return (g2_epis >> epi) & 1 ? pick_from(MODELS_G2, M, N) : pick_from(MODELS, M, N);
 }
 
 template <bool BF>
@@ -295,7 +295,6 @@ hipError_t gemm_cfg(bool bf16, int epi, int config, const GemmArgs& g, hipStream
   if (g.M <= 0 || g.N <= 0) return hipSuccess;
   if (g.K <= 0 || (g.K % BK) != 0 || (g.lda % 8) != 0 || (g.ldw % 8) != 0) return hipErrorInvalidValue;
   const int id = config >= 0 ? config : pick_config(epi, g.M, g.N);
-  if (epi == EPI_FILTER && id >= 11) return hipErrorInvalidValue;   // G2 has no filtered epilogue
   return bf16 ? dispatch<true>(epi, id, g, s) : dispatch<false>(epi, id, g, s);
 }
 

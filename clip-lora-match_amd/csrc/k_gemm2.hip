@@ -221,7 +221,8 @@ hipError_t by_epi(int epi, int id, const GemmArgs& g, hipStream_t s) {
     case EPI_RESID: return by_id<BF, EPI_RESID>(id, g, s);
     case EPI_PATCH: return by_id<BF, EPI_PATCH>(id, g, s);
     case EPI_SCORE: return by_id<BF, EPI_SCORE>(id, g, s);
-    default: return hipErrorInvalidValue;   // EPI_FILTER: gemm_kernel only
+    case EPI_FILTER: return by_id<BF, EPI_FILTER>(id, g, s);
+    default: return hipErrorInvalidValue;
   }
 }
 }  // namespace
