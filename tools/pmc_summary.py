@@ -12,9 +12,9 @@ import sys
 
 
 def short(name):
-    m = re.search(r"gemm_kernel<([^>]*)>", name)
+    m = re.search(r"(gemm2?_kernel)<([^>]*)>", name)
     if m:
-        return "gemm_kernel<" + m.group(1) + ">"
+        return m.group(1) + "<" + m.group(2) + ">"
     return re.sub(r"\(.*", "", name).replace("clm::(anonymous namespace)::", "").replace("void ", "")
 
 
@@ -38,7 +38,7 @@ def main(src="gpurun_out/pmc", tag="r01"):
         per_launch = (2 * sum(f) / len(f) + sum(w) / len(w)) * 1024
         out["kernels"][k] = {"launches": len(f), "hbm_bytes_per_launch": per_launch,
                              "fetch_bytes": 2 * sum(f) / len(f) * 1024, "write_bytes": sum(w) / len(w) * 1024}
-        if k.startswith("gemm_kernel"):
+        if k.startswith("gemm"):
             g_bytes += per_launch * len(f)
             g_n += len(f)
     out["gemm_mean_hbm_bytes_per_launch"] = g_bytes / max(g_n, 1)
