@@ -218,13 +218,13 @@ hipError_t launch_id(int id, const GemmArgs& g, hipStream_t s) {
     case 8: return launch_cfg<BF, EPI, 256, 128, 4, 2, 2>(g, s);
     case 9: return launch_cfg<BF, EPI, 192, 192, 2, 2, 2>(g, s);
     case 10: return launch_cfg<BF, EPI, 128, 256, 2, 4, 2>(g, s);
-    case 11: case 12: case 13: case 14: case 15: case 16: case 17: case 18:
+    case 11: case 12: case 13: case 14: case 15: case 16: case 17: case 18: case 19: case 20:
       return gemm2_launch(BF, EPI, id, g, s);
     default: return hipErrorInvalidValue;
   }
 }
 
-constexpr int NCFG = 19;
+constexpr int NCFG = 21;
 
 // Tile choice: a cost model per kernel family, time(cfg) ~ rounds(cfg) x round_cost(cfg),
 // rounds = ceil(tiles / resident workgroups), round_cost = BM*BN*(workgroups per CU) /
@@ -272,7 +272,18 @@ int pick_config(int epi, int M, int N) {
     const char* e = getenv("CLM_G2_EPIS");
     g2_epis = e ? atoi(e) : (1 << EPI_GELU);
   }
-  return (g2_epis >> epi) & 1 ? pick_from(MODELS_G2, M, N) : pick_from(MODELS, M, N);
+  // G2 16 / 18 -> their deferred-store twins 19 / 20 ($CLM_G2_DEFER=1). Off: spreading a
+  // tile's stores over the next tile's K-steps made fc1 7 % slower in the pipeline (the stores
+  // share the CU's memory path with the main loop's LDS-DMA), against the burst epilogue.
+  static int defer = -1;
+  if (defer < 0) {
+    const char* e = getenv("CLM_G2_DEFER");
+    defer = e ? atoi(e) : 0;
+  }
+  if (!((g2_epis >> epi) & 1)) return pick_from(MODELS, M, N);
+  const int id = pick_from(MODELS_G2, M, N);
+  if (defer && (epi == EPI_STORE || epi == EPI_GELU)) return id == 16 ? 19 : id == 18 ? 20 : id;
+  return id;
 }
 
 template <bool BF>

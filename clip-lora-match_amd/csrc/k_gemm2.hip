@@ -34,7 +34,7 @@ struct Cfg2 {
 
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
 
-template <bool BF, int EPI, int BM, int BN, int WM, int WN>
+template <bool BF, int EPI, int BM, int BN, int WM, int WN, bool DEFER>
 __global__ __launch_bounds__(WM * WN * 64, 1) void gemm2_kernel(GemmArgs g) {
   using C = Cfg2<BM, BN, WM, WN>;
   constexpr int TM = C::TM, TN = C::TN;
@@ -141,6 +141,23 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void gemm2_kernel(GemmArgs g) {
   constexpr int E0 = epi_min_stores<EPI, TM, TN>();
   constexpr int E = E0 > 63 ? 63 : E0;
   const bool vec_epi = (g.N % 4) == 0 && (g.ldo % 4) == 0 && !(g.debug & 1);
+  // DEFER (STORE / GELU, 16-B store path only): a tile's output is converted to packed
+  // 16-bit units at its end (bias, quick-GELU, pair swap) but stored one 1-KiB wave-store per
+  // K-step of the NEXT tile, so the per-CU store data path (~16 B/clk) drains beside that
+  // tile's MFMAs instead of in a burst the whole chip waits for.
+  constexpr int NU = DEFER ? TM * TN / 2 : 1;
+  static_assert(!DEFER || ((EPI == EPI_STORE || EPI == EPI_GELU) && TN % 2 == 0), "DEFER: 16-B store epilogues");
+  u32x4 pend[NU];
+  int pm0 = 0, pn0 = 0;
+  bool have = false, stored = false;
+  auto store_unit = [&](int u) {   // u: compile-time after unrolling
+    const int mb = u / (TN / 2), nb = (u % (TN / 2)) * 2, q = lane >> 4;
+    const int m = pm0 + wm * (BM / WM) + (lane & 15) + mb * 16;
+    const int col = pn0 + wn * (BN / WN) + (q & 1) * 16 + (q >> 1) * 8 + nb * 16;
+    const auto ob = buf_rsrc((const u16*)g.out + (int64_t)pm0 * g.ldo);
+    const uint32_t off = (m < g.M && col < g.N) ? (uint32_t)(((m - pm0) * g.ldo + col) * 2) : BUF_OOB;
+    __builtin_amdgcn_raw_buffer_store_b128(pend[u], ob, off, 0, 0);
+  };
   int s = 0;   // K-step of the ring (all tiles of this workgroup)
   for (int ti = 0; ti < n_my; ++ti) {
     int m0, n0;
@@ -153,31 +170,86 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void gemm2_kernel(GemmArgs g) {
       read_frags(smem + (s & 1) * C::STAGE_BYTES, 1, a1, b1);
       mma(a0, b0);
       if (s + 1 < S) {
-        // DMA(s+1) retired (only the previous tile's epilogue stores are younger), kk1
-        // fragments of s landed, and after the barrier no wave reads buffer s&1 any more
-        if (kt == 0 && ti > 0 && vec_epi) wait_vmcnt<E>();
-        else wait_vmcnt<0>();
+        // DMA(s+1) retired (only the stores issued after it -- the previous tile's epilogue,
+        // or one deferred unit -- are younger), kk1 fragments of s landed, and after the
+        // barrier no wave reads buffer s&1 any more
+        if constexpr (DEFER) {
+          if (stored) wait_vmcnt<1>();
+          else wait_vmcnt<0>();
+        } else {
+          if (kt == 0 && ti > 0 && vec_epi) wait_vmcnt<E>();
+          else wait_vmcnt<0>();
+        }
         lds_barrier();
         if (s + 2 < S) dma_next(s & 1);
         read_frags(smem + ((s + 1) & 1) * C::STAGE_BYTES, 0, a0, b0);
       }
       mma(a1, b1);
+      if constexpr (DEFER) {
+        stored = have && kt < NU;
+        if (stored) {
+#pragma unroll
+          for (int u = 0; u < NU; ++u)
+            if (u == kt) store_unit(u);
+        }
+      }
     }
     if (g.debug & 1) {
 #pragma unroll
       for (int mb = 0; mb < TM; ++mb)
 #pragma unroll
         for (int nb = 0; nb < TN; ++nb) asm volatile("" ::"v"(acc[mb][nb]));
+    } else if constexpr (DEFER) {
+      if (have && nk < NU) {   // short K: flush the units the loop did not reach
+#pragma unroll
+        for (int u = 0; u < NU; ++u)
+          if (u >= nk) store_unit(u);
+        stored = false;
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // keep the counted waits exact
+      }
+      const int q = lane >> 4;
+#pragma unroll
+      for (int mb = 0; mb < TM; ++mb) {
+#pragma unroll
+        for (int nb = 0; nb < TN; nb += 2) {
+          uint32_t w[2][2];
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            const int n = n0 + wn * (BN / WN) + (nb + h) * 16 + q * 4;
+            const float4 c = (g.bias && n < g.N) ? *(const float4*)(g.bias + n) : make_float4(0.f, 0.f, 0.f, 0.f);
+            float v[4] = {acc[mb][nb + h][0] + c.x, acc[mb][nb + h][1] + c.y, acc[mb][nb + h][2] + c.z,
+                          acc[mb][nb + h][3] + c.w};
+            if constexpr (EPI == EPI_GELU) {
+#pragma unroll
+              for (int j = 0; j < 4; ++j) v[j] = quick_gelu(v[j]);
+            }
+            w[h][0] = pack2<BF>(v[0], v[1]);
+            w[h][1] = pack2<BF>(v[2], v[3]);
+          }
+          const auto rx = __builtin_amdgcn_permlane16_swap(w[0][0], w[1][0], false, false);
+          const auto ry = __builtin_amdgcn_permlane16_swap(w[0][1], w[1][1], false, false);
+          pend[mb * (TN / 2) + nb / 2] = u32x4{rx[0], ry[0], rx[1], ry[1]};
+        }
+      }
+      pm0 = m0;
+      pn0 = n0;
+      have = true;
     } else {
       epilogue<BF, EPI, BM, BN, WM, WN, 2>(g, acc, m0, n0, wm, wn, lane);
     }
   }
+  if constexpr (DEFER) {
+    if (have) {
+#pragma unroll
+      for (int u = 0; u < NU; ++u) store_unit(u);
+    }
+  }
 }
 
-template <bool BF, int EPI, int BM, int BN, int WM, int WN>
+template <bool BF, int EPI, int BM, int BN, int WM, int WN, bool DEFER = false>
 hipError_t launch_cfg2(const GemmArgs& g, hipStream_t s) {
   using C = Cfg2<BM, BN, WM, WN>;
-  auto kern = gemm2_kernel<BF, EPI, BM, BN, WM, WN>;
+  auto kern = gemm2_kernel<BF, EPI, BM, BN, WM, WN, DEFER>;
   static unsigned dev_done = 0;
   int dev = 0;
   (void)hipGetDevice(&dev);
@@ -210,6 +282,12 @@ hipError_t by_id(int id, const GemmArgs& g, hipStream_t s) {
     case 16: return launch_cfg2<BF, EPI, 256, 128, 4, 2>(g, s);
     case 17: return launch_cfg2<BF, EPI, 192, 256, 2, 4>(g, s);
     case 18: return launch_cfg2<BF, EPI, 128, 256, 2, 4>(g, s);
+    case 19: case 20: {   // deferred-store variants of 16 / 18 (16-B store epilogues only)
+      constexpr bool D = EPI == EPI_STORE || EPI == EPI_GELU;
+      const bool wide = (g.N % 8) == 0 && (g.ldo % 8) == 0 && ((uintptr_t)g.out & 15) == 0;
+      if (id == 19) return D && wide ? launch_cfg2<BF, EPI, 256, 128, 4, 2, D>(g, s) : launch_cfg2<BF, EPI, 256, 128, 4, 2>(g, s);
+      return D && wide ? launch_cfg2<BF, EPI, 128, 256, 2, 4, D>(g, s) : launch_cfg2<BF, EPI, 128, 256, 2, 4>(g, s);
+    }
     default: return hipErrorInvalidValue;
   }
 }
