@@ -218,13 +218,13 @@ hipError_t launch_id(int id, const GemmArgs& g, hipStream_t s) {
     case 8: return launch_cfg<BF, EPI, 256, 128, 4, 2, 2>(g, s);
     case 9: return launch_cfg<BF, EPI, 192, 192, 2, 2, 2>(g, s);
     case 10: return launch_cfg<BF, EPI, 128, 256, 2, 4, 2>(g, s);
-    case 11: case 12: case 13: case 14: case 15: case 16: case 17: case 18: case 19: case 20:
+    case 11: case 12: case 13: case 14: case 15: case 16: case 17: case 18: case 19: case 20: case 21: case 22:
       return gemm2_launch(BF, EPI, id, g, s);
     default: return hipErrorInvalidValue;
   }
 }
 
-constexpr int NCFG = 21;
+constexpr int NCFG = 23;
 
 // Tile choice: a cost model per kernel family, time(cfg) ~ rounds(cfg) x round_cost(cfg),
 // rounds = ceil(tiles / resident workgroups), round_cost = BM*BN*(workgroups per CU) /
@@ -280,8 +280,14 @@ int pick_config(int epi, int M, int N) {
     const char* e = getenv("CLM_G2_DEFER");
     defer = e ? atoi(e) : 0;
   }
+  static int stages = -1;   // G2 16 / 18 -> their 3-buffer-ring twins 21 / 22; $CLM_G2_STAGES
+  if (stages < 0) {
+    const char* e = getenv("CLM_G2_STAGES");
+    stages = e ? atoi(e) : 2;
+  }
   if (!((g2_epis >> epi) & 1)) return pick_from(MODELS, M, N);
   const int id = pick_from(MODELS_G2, M, N);
+  if (stages == 3) return id == 16 ? 21 : id == 18 ? 22 : id;
   if (defer && (epi == EPI_STORE || epi == EPI_GELU)) return id == 16 ? 19 : id == 18 ? 20 : id;
   return id;
 }

@@ -19,14 +19,14 @@ using namespace gemm_detail;
 // The LDS latency of every fragment read is covered by 64 MFMAs of the other half, the only
 // MFMA-idle window per step is the barrier, and DMA(s+2) is issued before a tile end's
 // epilogue stores, so the next wait never drains them (counted vmcnt).
-template <int BM, int BN, int WM, int WN>
+template <int BM, int BN, int WM, int WN, int NS = 2>
 struct Cfg2 {
   static constexpr int NW = WM * WN;
   static constexpr int NT = NW * 64;
   static constexpr int TM = BM / WM / 16;
   static constexpr int TN = BN / WN / 16;
   static constexpr int STAGE_BYTES = (BM + BN) * BK * 2;
-  static constexpr int LDS = 2 * STAGE_BYTES;
+  static constexpr int LDS = NS * STAGE_BYTES;   // NS-buffer ring: DMA lead of NS-1 K-steps
   static constexpr int LA = BM / 8 / NW;
   static constexpr int LB = BN / 8 / NW;
   static_assert(BM % (8 * NW) == 0 && BN % (8 * NW) == 0, "rows must split evenly over waves");
@@ -34,9 +34,11 @@ struct Cfg2 {
 
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
 
-template <bool BF, int EPI, int BM, int BN, int WM, int WN, bool DEFER>
+template <bool BF, int EPI, int BM, int BN, int WM, int WN, bool DEFER, int NS>
 __global__ __launch_bounds__(WM * WN * 64, 1) void gemm2_kernel(GemmArgs g) {
-  using C = Cfg2<BM, BN, WM, WN>;
+  using C = Cfg2<BM, BN, WM, WN, NS>;
+  static_assert(NS == 2 || NS == 3, "ring of 2 or 3 buffers");
+  constexpr int L = C::LA + C::LB;   // vmcnt units (DMA instructions) per K-step
   constexpr int TM = C::TM, TN = C::TN;
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -128,12 +130,10 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void gemm2_kernel(GemmArgs g) {
   };
 
   dma_next(0);
-  if (S > 1) {
-    dma_next(1);
-    wait_vmcnt<C::LA + C::LB>();
-  } else {
-    wait_vmcnt<0>();
-  }
+  if (S > 1) dma_next(1);
+  if (NS == 3 && S > 2) dma_next(2);
+  if (S >= NS) wait_vmcnt<L * (NS - 1)>();   // DMA(0) retired, the younger ones in flight
+  else wait_vmcnt<0>();
   lds_barrier();
   u32x4 a0[TM], b0[TN], a1[TM], b1[TN];
   read_frags(smem, 0, a0, b0);
@@ -158,7 +158,8 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void gemm2_kernel(GemmArgs g) {
     const uint32_t off = (m < g.M && col < g.N) ? (uint32_t)(((m - pm0) * g.ldo + col) * 2) : BUF_OOB;
     __builtin_amdgcn_raw_buffer_store_b128(pend[u], ob, off, 0, 0);
   };
-  int s = 0;   // K-step of the ring (all tiles of this workgroup)
+  int s = 0;     // K-step of the ring (all tiles of this workgroup)
+  int cur = 0;   // its LDS buffer, s % NS
   for (int ti = 0; ti < n_my; ++ti) {
     int m0, n0;
     coords(ti, m0, n0);
@@ -167,24 +168,27 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void gemm2_kernel(GemmArgs g) {
 #pragma unroll
       for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
     for (int kt = 0; kt < nk; ++kt, ++s) {
-      read_frags(smem + (s & 1) * C::STAGE_BYTES, 1, a1, b1);
+      read_frags(smem + cur * C::STAGE_BYTES, 1, a1, b1);
       mma(a0, b0);
+      const int nxt = cur + 1 == NS ? 0 : cur + 1;
       if (s + 1 < S) {
-        // DMA(s+1) retired (only the stores issued after it -- the previous tile's epilogue,
-        // or one deferred unit -- are younger), kk1 fragments of s landed, and after the
-        // barrier no wave reads buffer s&1 any more
+        // DMA(s+1) retired -- younger: DMA(s+2) when NS = 3, and the stores issued after the
+        // DMAs of the previous step (a tile end's epilogue, or one deferred unit) -- kk1
+        // fragments of s landed, and after the barrier no wave reads buffer `cur` any more
+        const bool more = NS == 3 && s + 2 < S;
         if constexpr (DEFER) {
-          if (stored) wait_vmcnt<1>();
-          else wait_vmcnt<0>();
+          if (stored) { if (more) wait_vmcnt<L * (NS - 2) + 1>(); else wait_vmcnt<1>(); }
+          else { if (more) wait_vmcnt<L * (NS - 2)>(); else wait_vmcnt<0>(); }
         } else {
-          if (kt == 0 && ti > 0 && vec_epi) wait_vmcnt<E>();
-          else wait_vmcnt<0>();
+          if (kt == 0 && ti > 0 && vec_epi) { if (more) wait_vmcnt<L * (NS - 2) + E>(); else wait_vmcnt<E>(); }
+          else { if (more) wait_vmcnt<L * (NS - 2)>(); else wait_vmcnt<0>(); }
         }
         lds_barrier();
-        if (s + 2 < S) dma_next(s & 1);
-        read_frags(smem + ((s + 1) & 1) * C::STAGE_BYTES, 0, a0, b0);
+        if (s + NS < S) dma_next(cur);
+        read_frags(smem + nxt * C::STAGE_BYTES, 0, a0, b0);
       }
       mma(a1, b1);
+      cur = nxt;
       if constexpr (DEFER) {
         stored = have && kt < NU;
         if (stored) {
@@ -246,10 +250,10 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void gemm2_kernel(GemmArgs g) {
   }
 }
 
-template <bool BF, int EPI, int BM, int BN, int WM, int WN, bool DEFER = false>
+template <bool BF, int EPI, int BM, int BN, int WM, int WN, bool DEFER = false, int NS = 2>
 hipError_t launch_cfg2(const GemmArgs& g, hipStream_t s) {
-  using C = Cfg2<BM, BN, WM, WN>;
-  auto kern = gemm2_kernel<BF, EPI, BM, BN, WM, WN, DEFER>;
+  using C = Cfg2<BM, BN, WM, WN, NS>;
+  auto kern = gemm2_kernel<BF, EPI, BM, BN, WM, WN, DEFER, NS>;
   static unsigned dev_done = 0;
   int dev = 0;
   (void)hipGetDevice(&dev);
@@ -288,6 +292,8 @@ hipError_t by_id(int id, const GemmArgs& g, hipStream_t s) {
       if (id == 19) return D && wide ? launch_cfg2<BF, EPI, 256, 128, 4, 2, D>(g, s) : launch_cfg2<BF, EPI, 256, 128, 4, 2>(g, s);
       return D && wide ? launch_cfg2<BF, EPI, 128, 256, 2, 4, D>(g, s) : launch_cfg2<BF, EPI, 128, 256, 2, 4>(g, s);
     }
+    case 21: return launch_cfg2<BF, EPI, 256, 128, 4, 2, false, 3>(g, s);   // 3-buffer rings: 144 KiB
+    case 22: return launch_cfg2<BF, EPI, 128, 256, 2, 4, false, 3>(g, s);
     default: return hipErrorInvalidValue;
   }
 }

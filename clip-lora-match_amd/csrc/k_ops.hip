@@ -104,52 +104,70 @@ __global__ __launch_bounds__(256) void ln_kernel(LnArgs a) {
 // the memory instructions of the float2 form above; HBM-bound).
 template <bool BF, int NQ>
 __global__ __launch_bounds__(256) void ln4_kernel(LnArgs a) {
+  // R rows per wave (both rows' loads issued before either is reduced; gamma / beta loaded
+  // once per wave and reused)
+  constexpr int R = 2;
   const int lane = threadIdx.x & 63;
-  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (row >= a.M) return;
+  const int row0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * R;
+  if (row0 >= a.M) return;
   constexpr int d = NQ * 256;
-  float4 x[NQ];
-  if (a.mode == 0) {
-    const float* src = a.src + (int64_t)row * a.lds;
+  float4 x[R][NQ];
 #pragma unroll
-    for (int i = 0; i < NQ; ++i) x[i] = *(const float4*)(src + (i * 64 + lane) * 4);
-  } else {
-    const int tokid = a.ids[row];
-    const float* tk = a.tok + (int64_t)tokid * d;
-    const float* ps = a.pos + (int64_t)(row % a.L) * d;
+  for (int r = 0; r < R; ++r) {
+    const int row = min(row0 + r, a.M - 1);
+    if (a.mode == 0) {
+      const float* src = a.src + (int64_t)row * a.lds;
 #pragma unroll
-    for (int i = 0; i < NQ; ++i) {
-      const int e = (i * 64 + lane) * 4;
-      const float4 t = *(const float4*)(tk + e), p = *(const float4*)(ps + e);
-      x[i] = make_float4(t.x + p.x, t.y + p.y, t.z + p.z, t.w + p.w);
+      for (int i = 0; i < NQ; ++i) x[r][i] = *(const float4*)(src + (i * 64 + lane) * 4);
+    } else {
+      const int tokid = a.ids[row];
+      const float* tk = a.tok + (int64_t)tokid * d;
+      const float* ps = a.pos + (int64_t)(row % a.L) * d;
+#pragma unroll
+      for (int i = 0; i < NQ; ++i) {
+        const int e = (i * 64 + lane) * 4;
+        const float4 t = *(const float4*)(tk + e), p = *(const float4*)(ps + e);
+        x[r][i] = make_float4(t.x + p.x, t.y + p.y, t.z + p.z, t.w + p.w);
+      }
     }
   }
   auto ln = [&](const float* g, const float* b) {
-    float s = 0.f;
-#pragma unroll
-    for (int i = 0; i < NQ; ++i) s += (x[i].x + x[i].y) + (x[i].z + x[i].w);
-    const float mean = wave_sum(s) / d;
-    float v = 0.f;
+    float4 gg[NQ], bb[NQ];
 #pragma unroll
     for (int i = 0; i < NQ; ++i) {
-      const float d0 = x[i].x - mean, d1 = x[i].y - mean, d2 = x[i].z - mean, d3 = x[i].w - mean;
-      v += (d0 * d0 + d1 * d1) + (d2 * d2 + d3 * d3);
+      gg[i] = *(const float4*)(g + (i * 64 + lane) * 4);
+      bb[i] = *(const float4*)(b + (i * 64 + lane) * 4);
     }
-    const float rstd = 1.0f / sqrtf(wave_sum(v) / d + a.eps);
 #pragma unroll
-    for (int i = 0; i < NQ; ++i) {
-      const int e = (i * 64 + lane) * 4;
-      const float4 gg = *(const float4*)(g + e), bb = *(const float4*)(b + e);
-      x[i].x = (x[i].x - mean) * rstd * gg.x + bb.x;
-      x[i].y = (x[i].y - mean) * rstd * gg.y + bb.y;
-      x[i].z = (x[i].z - mean) * rstd * gg.z + bb.z;
-      x[i].w = (x[i].w - mean) * rstd * gg.w + bb.w;
+    for (int r = 0; r < R; ++r) {
+      float s = 0.f;
+#pragma unroll
+      for (int i = 0; i < NQ; ++i) s += (x[r][i].x + x[r][i].y) + (x[r][i].z + x[r][i].w);
+      const float mean = wave_sum(s) / d;
+      float v = 0.f;
+#pragma unroll
+      for (int i = 0; i < NQ; ++i) {
+        const float d0 = x[r][i].x - mean, d1 = x[r][i].y - mean, d2 = x[r][i].z - mean, d3 = x[r][i].w - mean;
+        v += (d0 * d0 + d1 * d1) + (d2 * d2 + d3 * d3);
+      }
+      const float rstd = 1.0f / sqrtf(wave_sum(v) / d + a.eps);
+#pragma unroll
+      for (int i = 0; i < NQ; ++i) {
+        x[r][i].x = (x[r][i].x - mean) * rstd * gg[i].x + bb[i].x;
+        x[r][i].y = (x[r][i].y - mean) * rstd * gg[i].y + bb[i].y;
+        x[r][i].z = (x[r][i].z - mean) * rstd * gg[i].z + bb[i].z;
+        x[r][i].w = (x[r][i].w - mean) * rstd * gg[i].w + bb[i].w;
+      }
     }
   };
   auto store_h = [&]() {
-    float* h = a.hf + (int64_t)row * a.ldh;
 #pragma unroll
-    for (int i = 0; i < NQ; ++i) *(float4*)(h + (i * 64 + lane) * 4) = x[i];
+    for (int r = 0; r < R; ++r) {
+      if (row0 + r >= a.M) break;
+      float* h = a.hf + (int64_t)(row0 + r) * a.ldh;
+#pragma unroll
+      for (int i = 0; i < NQ; ++i) *(float4*)(h + (i * 64 + lane) * 4) = x[r][i];
+    }
   };
   if (a.g2) {
     ln(a.g1, a.b1);
@@ -159,37 +177,41 @@ __global__ __launch_bounds__(256) void ln4_kernel(LnArgs a) {
     if (a.mode == 1) store_h();
     ln(a.g1, a.b1);
   }
-  u16* y = a.y + (int64_t)row * a.ldy;
 #pragma unroll
-  for (int i = 0; i < NQ; ++i)
-    *(u32x2*)(y + (i * 64 + lane) * 4) = u32x2{pack2<BF>(x[i].x, x[i].y), pack2<BF>(x[i].z, x[i].w)};
-
-  if (a.loraA) {  // y[:, d + j] = sum_e x_e * A[j, e]
-    float mine = 0.f;
-    for (int j = 0; j < a.r_ext; ++j) {
-      const float* A = a.loraA + (int64_t)j * d;
-      float s = 0.f;
+  for (int r = 0; r < R; ++r) {
+    if (row0 + r >= a.M) break;
+    u16* y = a.y + (int64_t)(row0 + r) * a.ldy;
 #pragma unroll
-      for (int i = 0; i < NQ; ++i) {
-        const float4 w = *(const float4*)(A + (i * 64 + lane) * 4);
-        s += (x[i].x * w.x + x[i].y * w.y) + (x[i].z * w.z + x[i].w * w.w);
+    for (int i = 0; i < NQ; ++i)
+      *(u32x2*)(y + (i * 64 + lane) * 4) = u32x2{pack2<BF>(x[r][i].x, x[r][i].y), pack2<BF>(x[r][i].z, x[r][i].w)};
+    if (a.loraA) {  // y[:, d + j] = sum_e x_e * A[j, e]
+      float mine = 0.f;
+      for (int j = 0; j < a.r_ext; ++j) {
+        const float* A = a.loraA + (int64_t)j * d;
+        float sj = 0.f;
+#pragma unroll
+        for (int i = 0; i < NQ; ++i) {
+          const float4 w = *(const float4*)(A + (i * 64 + lane) * 4);
+          sj += (x[r][i].x * w.x + x[r][i].y * w.y) + (x[r][i].z * w.z + x[r][i].w * w.w);
+        }
+        sj = wave_sum(sj);
+        if (lane == j) mine = sj;
       }
-      s = wave_sum(s);
-      if (lane == j) mine = s;
+      if (lane < a.r_pad) y[d + lane] = from_f32<BF>(lane < a.r_ext ? mine : 0.f);
     }
-    if (lane < a.r_pad) y[d + lane] = from_f32<BF>(lane < a.r_ext ? mine : 0.f);
   }
 }
 
 template <bool BF>
 hipError_t ln_dispatch(const LnArgs& a, hipStream_t s) {
   dim3 grid((a.M + 3) / 4), block(256);
+  dim3 grid2((a.M + 7) / 8);   // ln4_kernel: 2 rows per wave
   switch (a.d) {
     case 128: ln_kernel<BF, 1><<<grid, block, 0, s>>>(a); break;
-    case 256: ln4_kernel<BF, 1><<<grid, block, 0, s>>>(a); break;
-    case 512: ln4_kernel<BF, 2><<<grid, block, 0, s>>>(a); break;
-    case 768: ln4_kernel<BF, 3><<<grid, block, 0, s>>>(a); break;
-    case 1024: ln4_kernel<BF, 4><<<grid, block, 0, s>>>(a); break;
+    case 256: ln4_kernel<BF, 1><<<grid2, block, 0, s>>>(a); break;
+    case 512: ln4_kernel<BF, 2><<<grid2, block, 0, s>>>(a); break;
+    case 768: ln4_kernel<BF, 3><<<grid2, block, 0, s>>>(a); break;
+    case 1024: ln4_kernel<BF, 4><<<grid2, block, 0, s>>>(a); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();
