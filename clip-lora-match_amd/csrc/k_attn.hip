@@ -7,9 +7,9 @@
 // so the product is bit-identical to scaling the scores).
 //
 // One workgroup = (64-row query block, head, batch); 4 waves x 16 query rows.
-// Key tiles of 64: K staged in LDS with the 128-B-row XOR swizzle (conflict-free
-// ds_read_b128 B-fragments), V staged transposed (V^T rows of 144 B) so the PV
-// B-fragment is one ds_read_b128; online softmax in fp32 with 16-lane group
+// Key tiles of 64: K and V staged in LDS row-major with the 128-B-row XOR swizzle (K read
+// as ds_read_b128 B-fragments, V through ds_read_b64_tr_b16, see v_frag_tr); online softmax
+// in fp32 with 16-lane group
 // reductions on the MFMA C layout; P goes through a per-wave LDS tile to become
 // the A operand of PV.
 #include "kernels.hpp"
@@ -17,17 +17,34 @@
 namespace clm {
 
 namespace {
-constexpr int VT_STRIDE = 144;  // bytes per V^T row (64 keys * 2 B + 16 B pad)
+
+// PV B-operand (16x16x32: lane l holds V[key0 + (l>>4)*8 + 0..7][dim0 + (l&15)]) from a
+// ROW-MAJOR V tile ([64 keys][128 B], 16-B chunks XOR-swizzled by (key>>1)&7 like K) with two
+// ds_read_b64_tr_b16: per 16-lane group, lane 4q+p addresses key row q, dims 4p..4p+3, and lane
+// i receives dim i of the 4 rows. V is then staged with one 16-B LDS write per chunk, instead
+// of eight 8-way bank-conflicted 2-B writes into a transposed image.
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ u32x4 v_frag_tr(const uint8_t* tile, int kbase, int nb, int lane) {
+  const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
+  const int chunk = nb * 2 + (p >> 1);
+  const int ka = kbase + g * 8 + q, kb = ka + 4;
+  const uint8_t* pa = tile + ka * 128 + ((chunk ^ ((ka >> 1) & 7)) << 4) + (p & 1) * 8;
+  const uint8_t* pb = tile + kb * 128 + ((chunk ^ ((kb >> 1) & 7)) << 4) + (p & 1) * 8;
+  const s16x4 ra = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)pa);
+  const s16x4 rb = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)pb);
+  const u32x2 a = __builtin_bit_cast(u32x2, ra), b = __builtin_bit_cast(u32x2, rb);
+  return u32x4{a.x, a.y, b.x, b.y};
+}
 
 template <bool BF, bool CAUSAL>
 __global__ __launch_bounds__(256) void attn_kernel(const u16* qkv, int64_t ldq, u16* out, int64_t ldo,
                                                    int T, int d) {
-  __shared__ __attribute__((aligned(16))) uint8_t smem[8192 + 64 * VT_STRIDE + 4 * 2048];
+  __shared__ __attribute__((aligned(16))) uint8_t smem[8192 + 8192 + 4 * 2048];
   const int qb = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   uint8_t* sK = smem;
-  uint8_t* sV = smem + 8192;
-  uint8_t* sP = smem + 8192 + 64 * VT_STRIDE + wid * 2048;
+  uint8_t* sV = smem + 8192;   // [64 keys][128 B] swizzled, like sK
+  uint8_t* sP = smem + 16384 + wid * 2048;
   const u16* base = qkv + (int64_t)b * T * ldq;
   const int q0 = qb * 64 + wid * 16;
 
@@ -58,11 +75,7 @@ __global__ __launch_bounds__(256) void attn_kernel(const u16* qkv, int64_t ldq, 
         vv = *(const u32x4*)(rp + 2 * d);
       }
       *(u32x4*)(sK + key * 128 + swz(key, c) * 16) = kv;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        *(u16*)(sV + (c * 8 + 2 * e) * VT_STRIDE + key * 2) = (u16)(vv[e] & 0xffff);
-        *(u16*)(sV + (c * 8 + 2 * e + 1) * VT_STRIDE + key * 2) = (u16)(vv[e] >> 16);
-      }
+      *(u32x4*)(sV + key * 128 + swz(key, c) * 16) = vv;
     }
     __syncthreads();
 
@@ -121,11 +134,7 @@ __global__ __launch_bounds__(256) void attn_kernel(const u16* qkv, int64_t ldq, 
       const int row = lane & 15, c = kk * 4 + (lane >> 4);
       const u32x4 pa = *(const u32x4*)(sP + row * 128 + swz(row, c) * 16);
 #pragma unroll
-      for (int nb = 0; nb < 4; ++nb) {
-        const int dim = nb * 16 + (lane & 15);
-        const u32x4 vb = *(const u32x4*)(sV + dim * VT_STRIDE + (kk * 32 + 8 * (lane >> 4)) * 2);
-        o[nb] = mfma16<BF>(pa, vb, o[nb]);
-      }
+      for (int nb = 0; nb < 4; ++nb) o[nb] = mfma16<BF>(pa, v_frag_tr(sV, kk * 32, nb, lane), o[nb]);
     }
   }
 #pragma unroll
@@ -139,18 +148,17 @@ __global__ __launch_bounds__(256) void attn_kernel(const u16* qkv, int64_t ldq, 
   }
 }
 // T <= 128: one workgroup per (head, batch), ceil(T/16) waves x 16 query rows; all
-// key tiles (<= 2 x 64) staged once; V^T rows hold 128 keys (272-B stride).
-constexpr int VS2 = 272;
+// key tiles (<= 2 x 64) of K and V staged once.
 template <bool BF, bool CAUSAL>
 __global__ __launch_bounds__(512) void attn_small_kernel(const u16* qkv, int64_t ldq, u16* out, int64_t ldo,
                                                          int T, int d) {
-  __shared__ __attribute__((aligned(16))) uint8_t smem[2 * 8192 + 64 * VS2 + 8 * 2048];
+  __shared__ __attribute__((aligned(16))) uint8_t smem[2 * 8192 + 2 * 8192 + 8 * 2048];
   const int h = blockIdx.x, b = blockIdx.y;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int nthr = blockDim.x;
   uint8_t* sK = smem;                     // [2 tiles][64 keys][128 B] swizzled
-  uint8_t* sV = smem + 2 * 8192;          // [64 dims][128 keys] (+pad)
-  uint8_t* sP = smem + 2 * 8192 + 64 * VS2 + wid * 2048;
+  uint8_t* sV = smem + 2 * 8192;          // [2 tiles][64 keys][128 B] swizzled, like sK
+  uint8_t* sP = smem + 4 * 8192 + wid * 2048;
   const u16* base = qkv + (int64_t)b * T * ldq;
   const int ntiles = (T + 63) / 64;
   for (int ci = tid; ci < ntiles * 512; ci += nthr) {
@@ -163,11 +171,7 @@ __global__ __launch_bounds__(512) void attn_small_kernel(const u16* qkv, int64_t
     }
     const int kt = key >> 6, kr = key & 63;
     *(u32x4*)(sK + kt * 8192 + kr * 128 + swz(kr, c) * 16) = kv;
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      *(u16*)(sV + (c * 8 + 2 * e) * VS2 + key * 2) = (u16)(vv[e] & 0xffff);
-      *(u16*)(sV + (c * 8 + 2 * e + 1) * VS2 + key * 2) = (u16)(vv[e] >> 16);
-    }
+    *(u32x4*)(sV + kt * 8192 + kr * 128 + swz(kr, c) * 16) = vv;
   }
   const int q0 = wid * 16;
   u32x4 qa[2];
@@ -238,11 +242,7 @@ __global__ __launch_bounds__(512) void attn_small_kernel(const u16* qkv, int64_t
       const int row = lane & 15, c = kk * 4 + (lane >> 4);
       const u32x4 pa = *(const u32x4*)(sP + row * 128 + swz(row, c) * 16);
 #pragma unroll
-      for (int nb = 0; nb < 4; ++nb) {
-        const int dim = nb * 16 + (lane & 15);
-        const u32x4 vb = *(const u32x4*)(sV + dim * VS2 + (kt * 64 + kk * 32 + 8 * (lane >> 4)) * 2);
-        o[nb] = mfma16<BF>(pa, vb, o[nb]);
-      }
+      for (int nb = 0; nb < 4; ++nb) o[nb] = mfma16<BF>(pa, v_frag_tr(sV + kt * 8192, kk * 32, nb, lane), o[nb]);
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // P reads done before next tile's P writes
   }
