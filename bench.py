@@ -52,12 +52,16 @@ def flops_per_pair(cfg) -> dict:
         per_layer = 2 * T * d * (3 * d + d + 2 * mlp) + 4 * T * T * d + lora_w * T
         return L * per_layer
     r = cfg.lora_r
-    lora_tok = lambda d: 2 * 4 * (2 * r * d)  # q,k,v,out: x.A^T (r x d) + (.)B^T (d x r)
+
+    def lora_tok(d, mlp):   # per token and layer: x.A^T (r x fin) + (.)B^T (fout x r) per target
+        dims = {"q_proj": (d, d), "k_proj": (d, d), "v_proj": (d, d), "out_proj": (d, d),
+                "fc1": (d, mlp), "fc2": (mlp, d)}
+        return sum(2 * r * (dims[t][0] + dims[t][1]) for t in cfg.lora_targets if t in dims)
     v, t = cfg.vision, cfg.text
     P = cfg.num_patches
-    img = tower(v.hidden, v.layers, v.mlp, P + 1, lora_tok(v.hidden)) \
+    img = tower(v.hidden, v.layers, v.mlp, P + 1, lora_tok(v.hidden, v.mlp)) \
         + 2 * P * (cfg.channels * cfg.patch ** 2) * v.hidden + 2 * v.hidden * cfg.proj_dim
-    txt = tower(t.hidden, t.layers, t.mlp, cfg.max_pos, lora_tok(t.hidden)) + 2 * t.hidden * cfg.proj_dim
+    txt = tower(t.hidden, t.layers, t.mlp, cfg.max_pos, lora_tok(t.hidden, t.mlp)) + 2 * t.hidden * cfg.proj_dim
     return {"image": float(img), "caption": float(txt)}
 
 
@@ -133,6 +137,42 @@ def search_leg(rows: int, queries: int, k: int, device):
             "index_dtype": "fp16", "tflops": flops / dt / 1e12}
 
 
+def l14_leg(device, batch: int = 128, steps: int = 3, warmup: int = 1):
+    """BASELINE configs[3]: ViT-L/14@336 + LoRA r=16 on q,k,v,out,fc1,fc2 (merged), bf16, image
+    tower, batch 128 (576 patches + CLS per image: the large-tile MFMA path). Synthetic weights
+    and uint8 336x336 images; inputs resident in HBM; one JSON sub-object."""
+    cfg = clm.get_preset("ViT-L/14@336")
+    sd, lora = W.synthetic_state_dict(cfg, 0), W.synthetic_lora(cfg, 1)
+    m = ClipLoraModel(cfg, device=device, compute_dtype="bfloat16", lora_mode="merged", max_batch=batch)
+    m.load_tensors(sd)
+    m.load_tensors(lora)
+    m.finalize()
+    del sd, lora
+    imgs = torch.from_numpy(syn.images_u8(batch, cfg.image_size, 4321)).to(device)
+    out = torch.empty((batch, cfg.proj_dim), dtype=torch.float32, device=device)
+    for _ in range(warmup):
+        m.encode_pixels(imgs, out=out)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        m.encode_pixels(imgs, out=out)
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / steps
+    m.prof_enable(True)
+    m.encode_pixels(imgs, out=out)
+    torch.cuda.synchronize()
+    prof = m.prof_read()
+    m.prof_enable(False)
+    m.close()
+    fp = flops_per_pair(cfg)["image"]
+    g_ms, g_flops, _ = prof["gemm"]
+    return {"config": "ViT-L/14@336 + LoRA r=16 (q,k,v,out,fc1,fc2) merged, bf16, batch 128, image tower",
+            "images_per_s": round(batch / dt, 1), "ms_per_step": round(dt * 1e3, 3),
+            "step_tflops": round(batch * fp / dt / 1e12, 1),
+            "gemm_tflops": round(g_flops / (g_ms * 1e-3) / 1e12, 1),
+            "kernel_ms": {k: round(v[0], 3) for k, v in prof.items()}}
+
+
 def pmc_traffic():
     """HBM bytes per GEMM launch from the newest committed PMC summary (tools/pmc_summary.py),
     or None when no counter run has been recorded."""
@@ -157,6 +197,7 @@ def main():
     ap.add_argument("--search-rows", type=int, default=10_000_000)
     ap.add_argument("--search-queries", type=int, default=10_000)
     ap.add_argument("--no-search", action="store_true")
+    ap.add_argument("--no-l14", action="store_true", help="skip the ViT-L/14@336 (configs[3]) leg")
     ap.add_argument("--sequential", action="store_true", help="towers back to back on one stream, no graph")
     ap.add_argument("--split", type=int, default=0, help="sub-batches per tower in encode_pair (0 = library default)")
     args = ap.parse_args()
@@ -273,6 +314,11 @@ def main():
             result["search"] = search_leg(args.search_rows, args.search_queries, 5, dev)
         except Exception as e:  # report, never hide
             result["search"] = {"error": repr(e)}
+    if rank == 0 and world == 1 and not args.no_l14:
+        try:
+            result["l14"] = l14_leg(dev)
+        except Exception as e:  # report, never hide
+            result["l14"] = {"error": repr(e)}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(cfg, sd, lora, args.cpu_budget)
     if rank == 0:
