@@ -6,28 +6,29 @@
 // The 64^-1/2 scale is folded into the q_proj weights at load (a power of two,
 // so the product is bit-identical to scaling the scores).
 //
-// One workgroup = (64-row query block, head, batch); 4 waves x 16 query rows.
 // Key tiles of 64: K and V staged in LDS row-major with the 128-B-row XOR swizzle (K read
-// as ds_read_b128 B-fragments, V through ds_read_b64_tr_b16, see v_frag_tr); online softmax
-// in fp32 with 16-lane group
-// reductions on the MFMA C layout; P goes through a per-wave LDS tile to become
-// the A operand of PV.
+// as ds_read_b128 fragments, V through ds_read_b64_tr_b16, see v_frag_trT). Scores are
+// computed transposed, S^T = K Q^T, so each lane owns one query: the fp32 softmax reduces
+// in-lane plus two cross-lane steps, and P stays in registers as the B operand of
+// O^T = V^T P^T. attn_kernel (T > 128) runs an online softmax over double-buffered tiles;
+// attn_small_kernel (T <= 128) holds every key and does one exact pass.
 #include "kernels.hpp"
 
 namespace clm {
 
 namespace {
 
-// PV B-operand (16x16x32: lane l holds V[key0 + (l>>4)*8 + 0..7][dim0 + (l&15)]) from a
-// ROW-MAJOR V tile ([64 keys][128 B], 16-B chunks XOR-swizzled by (key>>1)&7 like K) with two
-// ds_read_b64_tr_b16: per 16-lane group, lane 4q+p addresses key row q, dims 4p..4p+3, and lane
-// i receives dim i of the 4 rows. V is then staged with one 16-B LDS write per chunk, instead
-// of eight 8-way bank-conflicted 2-B writes into a transposed image.
 typedef short s16x4 __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ u32x4 v_frag_tr(const uint8_t* tile, int kbase, int nb, int lane) {
+
+// V^T operand of O^T = V^T P^T, from a ROW-MAJOR V tile ([64 keys][128 B], 16-B chunks
+// XOR-swizzled by (key>>1)&7 like K) with two ds_read_b64_tr_b16 (per 16-lane group, lane
+// 4q+p addresses key row q, dims 4p..4p+3, and lane i receives dim i of the 4 rows): lane l holds
+// V[key0 + 4*(l>>4) + 0..3][dim0 + (l&15)] and V[key0 + 16 + 4*(l>>4) + 0..3][dim0 + (l&15)],
+// the key order in which the lane holds P (S^T C layout of key blocks 2kk and 2kk+1).
+__device__ __forceinline__ u32x4 v_frag_trT(const uint8_t* tile, int kbase, int nb, int lane) {
   const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
   const int chunk = nb * 2 + (p >> 1);
-  const int ka = kbase + g * 8 + q, kb = ka + 4;
+  const int ka = kbase + g * 4 + q, kb = ka + 16;
   const uint8_t* pa = tile + ka * 128 + ((chunk ^ ((ka >> 1) & 7)) << 4) + (p & 1) * 8;
   const uint8_t* pb = tile + kb * 128 + ((chunk ^ ((kb >> 1) & 7)) << 4) + (p & 1) * 8;
   const s16x4 ra = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)pa);
@@ -36,129 +37,182 @@ __device__ __forceinline__ u32x4 v_frag_tr(const uint8_t* tile, int kbase, int n
   return u32x4{a.x, a.y, b.x, b.y};
 }
 
+// T > 128 (ViT-L/14@336: T = 577). One workgroup = (128-query block, head, batch): 4 waves x
+// two 16-query blocks, so every K fragment (ds_read_b128) and V fragment (ds_read_b64_tr_b16)
+// read from LDS feeds two MFMAs. Scores are computed transposed, S^T = K Q^T, so a lane owns
+// ONE query and 16 of the tile's 64 keys: the softmax max / sum are 15 in-lane ops + 2
+// cross-lane steps, and P stays in registers as the B operand of O^T = V^T P^T (no LDS round
+// trip). K / V tiles of 64 keys are double-buffered in LDS and the next tile is loaded into
+// registers while the current one computes: one barrier per tile.
 template <bool BF, bool CAUSAL>
-__global__ __launch_bounds__(256) void attn_kernel(const u16* qkv, int64_t ldq, u16* out, int64_t ldo,
-                                                   int T, int d) {
-  __shared__ __attribute__((aligned(16))) uint8_t smem[8192 + 8192 + 4 * 2048];
+__global__ __launch_bounds__(256, CAUSAL ? 2 : 3) void attn_kernel(const u16* qkv, int64_t ldq, u16* out, int64_t ldo,
+                                                      int T, int d) {
+  constexpr int RB = 2;   // 16-query blocks per wave
+  constexpr float L2E = 1.4426950408889634f;
+  __shared__ __attribute__((aligned(16))) uint8_t smem[2 * 16384];
   const int qb = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  uint8_t* sK = smem;
-  uint8_t* sV = smem + 8192;   // [64 keys][128 B] swizzled, like sK
-  uint8_t* sP = smem + 16384 + wid * 2048;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, g = lane >> 4;
   const u16* base = qkv + (int64_t)b * T * ldq;
-  const int q0 = qb * 64 + wid * 16;
+  const int qw = qb * 64 * RB + wid * 16 * RB;   // first query of this wave
 
-  u32x4 qa[2];
-  {
-    const int r = min(q0 + (lane & 15), T - 1);
+  u32x4 qa[RB][2];
+#pragma unroll
+  for (int rb = 0; rb < RB; ++rb) {
+    const int r = min(qw + rb * 16 + (lane & 15), T - 1);
     const u16* qp = base + (int64_t)r * ldq + h * 64;
 #pragma unroll
-    for (int kk = 0; kk < 2; ++kk) qa[kk] = *(const u32x4*)(qp + kk * 32 + 8 * (lane >> 4));
+    for (int kk = 0; kk < 2; ++kk) qa[rb][kk] = *(const u32x4*)(qp + kk * 32 + 8 * g);
   }
-  f32x4 o[4];
-  float mrow[4], lrow[4];
+  f32x4 o[RB][4];   // O^T: lane holds query (lane&15), dims nb*16 + 4g + 0..3
+  float mrow[RB], lrow[RB];   // running max (log2 domain) and sum for this lane's query
 #pragma unroll
-  for (int j = 0; j < 4; ++j) { o[j] = f32x4{0.f, 0.f, 0.f, 0.f}; mrow[j] = -INFINITY; lrow[j] = 0.f; }
+  for (int rb = 0; rb < RB; ++rb) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) o[rb][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    mrow[rb] = -INFINITY;
+    lrow[rb] = 0.f;
+  }
 
   const int ntiles = (T + 63) / 64;
-  const int nkt = CAUSAL ? min(qb + 1, ntiles) : ntiles;
-  for (int kt = 0; kt < nkt; ++kt) {
-    __syncthreads();
+  const int nkt = CAUSAL ? min((qb * 64 * RB + 64 * RB - 1) / 64 + 1, ntiles) : ntiles;
+  u32x4 kr[2], vr[2];   // this thread's 2 chunks of the next K / V tile
+  auto load = [&](int kt) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int ci = tid + 256 * i, key = ci >> 3, c = ci & 7, kg = kt * 64 + key;
+      kr[i] = u32x4{0u, 0u, 0u, 0u};
+      vr[i] = u32x4{0u, 0u, 0u, 0u};
+      if (kg < T) {
+        const u16* rp = base + (int64_t)kg * ldq + h * 64 + c * 8;
+        kr[i] = *(const u32x4*)(rp + d);
+        vr[i] = *(const u32x4*)(rp + 2 * d);
+      }
+    }
+  };
+  auto stage = [&](int buf) {
+    uint8_t* sK = smem + buf * 16384;
+    uint8_t* sV = sK + 8192;
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       const int ci = tid + 256 * i, key = ci >> 3, c = ci & 7;
-      const int kg = kt * 64 + key;
-      u32x4 kv = u32x4{0u, 0u, 0u, 0u}, vv = u32x4{0u, 0u, 0u, 0u};
-      if (kg < T) {
-        const u16* rp = base + (int64_t)kg * ldq + h * 64 + c * 8;
-        kv = *(const u32x4*)(rp + d);
-        vv = *(const u32x4*)(rp + 2 * d);
-      }
-      *(u32x4*)(sK + key * 128 + swz(key, c) * 16) = kv;
-      *(u32x4*)(sV + key * 128 + swz(key, c) * 16) = vv;
+      *(u32x4*)(sK + key * 128 + swz(key, c) * 16) = kr[i];
+      *(u32x4*)(sV + key * 128 + swz(key, c) * 16) = vr[i];
     }
-    __syncthreads();
-
-    f32x4 sc[4];
+  };
+  load(0);
+  stage(0);
+  if (nkt > 1) load(1);
+  __syncthreads();
+  for (int kt = 0; kt < nkt; ++kt) {
+    const uint8_t* sK = smem + (kt & 1) * 16384;
+    const uint8_t* sV = sK + 8192;
+    f32x4 sc[RB][4];   // S^T: lane holds query (lane&15), keys kt*64 + nb*16 + 4g + 0..3
 #pragma unroll
     for (int nb = 0; nb < 4; ++nb) {
-      sc[nb] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int rb = 0; rb < RB; ++rb) sc[rb][nb] = f32x4{0.f, 0.f, 0.f, 0.f};
       const int krow = nb * 16 + (lane & 15);
 #pragma unroll
       for (int kk = 0; kk < 2; ++kk) {
-        const int c = kk * 4 + (lane >> 4);
+        const int c = kk * 4 + g;
         const u32x4 kb = *(const u32x4*)(sK + krow * 128 + swz(krow, c) * 16);
-        sc[nb] = mfma16<BF>(qa[kk], kb, sc[nb]);
+#pragma unroll
+        for (int rb = 0; rb < RB; ++rb) sc[rb][nb] = mfma16<BF>(kb, qa[rb][kk], sc[rb][nb]);
       }
     }
+    const bool masked = CAUSAL || (kt + 1) * 64 > T;
+    u32x4 pb[RB][2];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int qi = q0 + (lane >> 4) * 4 + j;
-      float tmax = -INFINITY;
+    for (int rb = 0; rb < RB; ++rb) {
+      if (masked) {
+        const int qi = qw + rb * 16 + (lane & 15);
 #pragma unroll
-      for (int nb = 0; nb < 4; ++nb) {
-        const int kj = kt * 64 + nb * 16 + (lane & 15);
-        const bool ok = kj < T && (!CAUSAL || kj <= qi);
-        const float v = ok ? sc[nb][j] : -INFINITY;
-        sc[nb][j] = v;
-        tmax = fmaxf(tmax, v);
+        for (int nb = 0; nb < 4; ++nb)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int kj = kt * 64 + nb * 16 + 4 * g + j;
+            if (!(kj < T && (!CAUSAL || kj <= qi))) sc[rb][nb][j] = -INFINITY;
+          }
       }
-      tmax = group16_max(tmax);
-      const float mnew = fmaxf(mrow[j], tmax);
-      const float alpha = (mrow[j] == -INFINITY) ? 0.f : __expf(mrow[j] - mnew);
-      mrow[j] = mnew;
+      float tmax = sc[rb][0][0];
+#pragma unroll
+      for (int nb = 0; nb < 4; ++nb)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) tmax = fmaxf(tmax, sc[rb][nb][j]);
+      tmax = fmaxf(tmax, __shfl_xor(tmax, 16));
+      tmax = fmaxf(tmax, __shfl_xor(tmax, 32));
+      const float mnew = fmaxf(mrow[rb], tmax * L2E);
+      const float muse = mnew == -INFINITY ? 0.f : mnew;
+      const float alpha = __builtin_amdgcn_exp2f(mrow[rb] - muse);
+      mrow[rb] = mnew;
       float rs = 0.f;
 #pragma unroll
-      for (int nb = 0; nb < 4; ++nb) {
-        const float p = __expf(sc[nb][j] - mnew);
-        sc[nb][j] = p;
-        rs += p;
+      for (int nb = 0; nb < 4; ++nb)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const float p = __builtin_amdgcn_exp2f(fmaf(sc[rb][nb][j], L2E, -muse));
+          sc[rb][nb][j] = p;
+          rs += p;
+        }
+      rs += __shfl_xor(rs, 16);
+      rs += __shfl_xor(rs, 32);
+      lrow[rb] = lrow[rb] * alpha + rs;
+#pragma unroll
+      for (int nb = 0; nb < 4; ++nb)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) o[rb][nb][j] *= alpha;
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        const f32x4 lo = sc[rb][2 * kk], hi = sc[rb][2 * kk + 1];
+        pb[rb][kk] = u32x4{pack2<BF>(lo[0], lo[1]), pack2<BF>(lo[2], lo[3]),
+                           pack2<BF>(hi[0], hi[1]), pack2<BF>(hi[2], hi[3])};
       }
-      rs = group16_sum(rs);
-      lrow[j] = lrow[j] * alpha + rs;
-#pragma unroll
-      for (int nb = 0; nb < 4; ++nb) o[nb][j] *= alpha;
     }
-    // P (C layout: row=(lane>>4)*4+j, key=nb*16+(lane&15)) -> per-wave LDS [16][64]
-#pragma unroll
-    for (int nb = 0; nb < 4; ++nb) {
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int row = (lane >> 4) * 4 + j, key = nb * 16 + (lane & 15);
-        *(u16*)(sP + row * 128 + swz(row, key >> 3) * 16 + (key & 7) * 2) = from_f32<BF>(sc[nb][j]);
-      }
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
-      const int row = lane & 15, c = kk * 4 + (lane >> 4);
-      const u32x4 pa = *(const u32x4*)(sP + row * 128 + swz(row, c) * 16);
 #pragma unroll
-      for (int nb = 0; nb < 4; ++nb) o[nb] = mfma16<BF>(pa, v_frag_tr(sV, kk * 32, nb, lane), o[nb]);
+      for (int nb = 0; nb < 4; ++nb) {
+        const u32x4 va = v_frag_trT(sV, kk * 32, nb, lane);
+#pragma unroll
+        for (int rb = 0; rb < RB; ++rb) o[rb][nb] = mfma16<BF>(va, pb[rb][kk], o[rb][nb]);
+      }
     }
+    // publish tile kt+1 (loaded during this tile) into the other buffer -- every wave finished
+    // reading that buffer (tile kt-1) before the previous barrier -- and start loading kt+2
+    if (kt + 1 < nkt) {
+      stage((kt + 1) & 1);
+      if (kt + 2 < nkt) load(kt + 2);
+    }
+    __syncthreads();
   }
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int qi = q0 + (lane >> 4) * 4 + j;
+  for (int rb = 0; rb < RB; ++rb) {
+    const int qi = qw + rb * 16 + (lane & 15);
     if (qi >= T) continue;
-    const float inv = 1.0f / lrow[j];
-    u16* op = out + ((int64_t)b * T + qi) * ldo + h * 64 + (lane & 15);
+    const float inv = 1.0f / lrow[rb];
+    u16* op = out + ((int64_t)b * T + qi) * ldo + h * 64 + 4 * g;
 #pragma unroll
-    for (int nb = 0; nb < 4; ++nb) op[nb * 16] = from_f32<BF>(o[nb][j] * inv);
+    for (int nb = 0; nb < 4; ++nb)
+      *(u32x2*)(op + nb * 16) = u32x2{pack2<BF>(o[rb][nb][0] * inv, o[rb][nb][1] * inv),
+                                      pack2<BF>(o[rb][nb][2] * inv, o[rb][nb][3] * inv)};
   }
 }
-// T <= 128: one workgroup per (head, batch), ceil(T/16) waves x 16 query rows; all
-// key tiles (<= 2 x 64) of K and V staged once.
+
+// T <= 128 (ViT-B/32: vision T = 50, text T = 77 causal): one workgroup per (head, batch),
+// ceil(T/16) waves x 16 queries; all key tiles (<= 2 x 64) of K and V staged once. Scores are
+// transposed as in attn_kernel (lane = one query, 16 keys per tile), and since every key is
+// resident the softmax is a single exact pass over <= 32 in-lane values: no online rescale,
+// P straight from registers into O^T = V^T P^T.
 template <bool BF, bool CAUSAL>
 __global__ __launch_bounds__(512) void attn_small_kernel(const u16* qkv, int64_t ldq, u16* out, int64_t ldo,
                                                          int T, int d) {
-  __shared__ __attribute__((aligned(16))) uint8_t smem[2 * 8192 + 2 * 8192 + 8 * 2048];
+  constexpr float L2E = 1.4426950408889634f;
+  __shared__ __attribute__((aligned(16))) uint8_t smem[2 * 8192 + 2 * 8192];
   const int h = blockIdx.x, b = blockIdx.y;
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, g = lane >> 4;
   const int nthr = blockDim.x;
   uint8_t* sK = smem;                     // [2 tiles][64 keys][128 B] swizzled
   uint8_t* sV = smem + 2 * 8192;          // [2 tiles][64 keys][128 B] swizzled, like sK
-  uint8_t* sP = smem + 4 * 8192 + wid * 2048;
   const u16* base = qkv + (int64_t)b * T * ldq;
   const int ntiles = (T + 63) / 64;
   for (int ci = tid; ci < ntiles * 512; ci += nthr) {
@@ -173,88 +227,76 @@ __global__ __launch_bounds__(512) void attn_small_kernel(const u16* qkv, int64_t
     *(u32x4*)(sK + kt * 8192 + kr * 128 + swz(kr, c) * 16) = kv;
     *(u32x4*)(sV + kt * 8192 + kr * 128 + swz(kr, c) * 16) = vv;
   }
-  const int q0 = wid * 16;
+  const int q0 = wid * 16, qi = q0 + (lane & 15);
   u32x4 qa[2];
   {
-    const int r = min(q0 + (lane & 15), T - 1);
-    const u16* qp = base + (int64_t)r * ldq + h * 64;
+    const u16* qp = base + (int64_t)min(qi, T - 1) * ldq + h * 64;
 #pragma unroll
-    for (int kk = 0; kk < 2; ++kk) qa[kk] = *(const u32x4*)(qp + kk * 32 + 8 * (lane >> 4));
+    for (int kk = 0; kk < 2; ++kk) qa[kk] = *(const u32x4*)(qp + kk * 32 + 8 * g);
   }
   __syncthreads();
-  f32x4 o[4];
-  float mrow[4], lrow[4];
-#pragma unroll
-  for (int j = 0; j < 4; ++j) { o[j] = f32x4{0.f, 0.f, 0.f, 0.f}; mrow[j] = -INFINITY; lrow[j] = 0.f; }
   const int nkt = CAUSAL ? min((q0 + 15) / 64 + 1, ntiles) : ntiles;
-  for (int kt = 0; kt < nkt; ++kt) {
+  f32x4 sc[2][4];   // S^T: lane holds query qi, keys kt*64 + nb*16 + 4g + 0..3
+  float tmax = -INFINITY;
+#pragma unroll
+  for (int kt = 0; kt < 2; ++kt) {
+    if (kt >= nkt) break;
     const uint8_t* tK = sK + kt * 8192;
-    f32x4 sc[4];
 #pragma unroll
     for (int nb = 0; nb < 4; ++nb) {
-      sc[nb] = f32x4{0.f, 0.f, 0.f, 0.f};
+      sc[kt][nb] = f32x4{0.f, 0.f, 0.f, 0.f};
       const int krow = nb * 16 + (lane & 15);
 #pragma unroll
       for (int kk = 0; kk < 2; ++kk) {
-        const int c = kk * 4 + (lane >> 4);
-        sc[nb] = mfma16<BF>(qa[kk], *(const u32x4*)(tK + krow * 128 + swz(krow, c) * 16), sc[nb]);
+        const int c = kk * 4 + g;
+        sc[kt][nb] = mfma16<BF>(*(const u32x4*)(tK + krow * 128 + swz(krow, c) * 16), qa[kk], sc[kt][nb]);
       }
-    }
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int qi = q0 + (lane >> 4) * 4 + j;
-      float tmax = -INFINITY;
-#pragma unroll
-      for (int nb = 0; nb < 4; ++nb) {
-        const int kj = kt * 64 + nb * 16 + (lane & 15);
-        const bool ok = kj < T && (!CAUSAL || kj <= qi);
-        const float v = ok ? sc[nb][j] : -INFINITY;
-        sc[nb][j] = v;
-        tmax = fmaxf(tmax, v);
-      }
-      tmax = group16_max(tmax);
-      const float mnew = fmaxf(mrow[j], tmax);
-      const float alpha = (mrow[j] == -INFINITY) ? 0.f : __expf(mrow[j] - mnew);
-      mrow[j] = mnew;
-      float rs = 0.f;
-#pragma unroll
-      for (int nb = 0; nb < 4; ++nb) {
-        const float p = __expf(sc[nb][j] - mnew);
-        sc[nb][j] = p;
-        rs += p;
-      }
-      rs = group16_sum(rs);
-      lrow[j] = lrow[j] * alpha + rs;
-#pragma unroll
-      for (int nb = 0; nb < 4; ++nb) o[nb][j] *= alpha;
-    }
-#pragma unroll
-    for (int nb = 0; nb < 4; ++nb) {
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        const int row = (lane >> 4) * 4 + j, key = nb * 16 + (lane & 15);
-        *(u16*)(sP + row * 128 + swz(row, key >> 3) * 16 + (key & 7) * 2) = from_f32<BF>(sc[nb][j]);
+        const int kj = kt * 64 + nb * 16 + 4 * g + j;
+        if (!(kj < T && (!CAUSAL || kj <= qi))) sc[kt][nb][j] = -INFINITY;
+        tmax = fmaxf(tmax, sc[kt][nb][j]);
       }
     }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  }
+  tmax = fmaxf(tmax, __shfl_xor(tmax, 16));
+  tmax = fmaxf(tmax, __shfl_xor(tmax, 32));
+  const float m2 = tmax * L2E;   // key 0 is always visible: finite
+  float rs = 0.f;
+  f32x4 o[4];
+#pragma unroll
+  for (int nb = 0; nb < 4; ++nb) o[nb] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int kt = 0; kt < 2; ++kt) {
+    if (kt >= nkt) break;
+    u32x4 pb[2];
+#pragma unroll
+    for (int nb = 0; nb < 4; ++nb)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float p = __builtin_amdgcn_exp2f(fmaf(sc[kt][nb][j], L2E, -m2));
+        sc[kt][nb][j] = p;
+        rs += p;
+      }
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
-      const int row = lane & 15, c = kk * 4 + (lane >> 4);
-      const u32x4 pa = *(const u32x4*)(sP + row * 128 + swz(row, c) * 16);
-#pragma unroll
-      for (int nb = 0; nb < 4; ++nb) o[nb] = mfma16<BF>(pa, v_frag_tr(sV + kt * 8192, kk * 32, nb, lane), o[nb]);
+      const f32x4 lo = sc[kt][2 * kk], hi = sc[kt][2 * kk + 1];
+      pb[kk] = u32x4{pack2<BF>(lo[0], lo[1]), pack2<BF>(lo[2], lo[3]), pack2<BF>(hi[0], hi[1]),
+                     pack2<BF>(hi[2], hi[3])};
     }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // P reads done before next tile's P writes
-  }
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int qi = q0 + (lane >> 4) * 4 + j;
-    if (qi >= T) continue;
-    const float inv = 1.0f / lrow[j];
-    u16* op = out + ((int64_t)b * T + qi) * ldo + h * 64 + (lane & 15);
+    for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
-    for (int nb = 0; nb < 4; ++nb) op[nb * 16] = from_f32<BF>(o[nb][j] * inv);
+      for (int nb = 0; nb < 4; ++nb) o[nb] = mfma16<BF>(v_frag_trT(sV + kt * 8192, kk * 32, nb, lane), pb[kk], o[nb]);
   }
+  rs += __shfl_xor(rs, 16);
+  rs += __shfl_xor(rs, 32);
+  if (qi >= T) return;
+  const float inv = 1.0f / rs;
+  u16* op = out + ((int64_t)b * T + qi) * ldo + h * 64 + 4 * g;
+#pragma unroll
+  for (int nb = 0; nb < 4; ++nb)
+    *(u32x2*)(op + nb * 16) = u32x2{pack2<BF>(o[nb][0] * inv, o[nb][1] * inv), pack2<BF>(o[nb][2] * inv, o[nb][3] * inv)};
 }
 }  // namespace
 
@@ -273,7 +315,7 @@ hipError_t attention(bool bf16, bool causal, const u16* qkv, int64_t ldq, u16* o
     }
     return hipGetLastError();
   }
-  dim3 grid((T + 63) / 64, H, B), block(256);
+  dim3 grid((T + 127) / 128, H, B), block(256);
   if (bf16) {
     if (causal) attn_kernel<true, true><<<grid, block, 0, s>>>(qkv, ldq, out, ldo, T, d);
     else attn_kernel<true, false><<<grid, block, 0, s>>>(qkv, ldq, out, ldo, T, d);
