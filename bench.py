@@ -45,37 +45,55 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def flops_per_pair(cfg) -> dict:
+def pruned_last_layer() -> bool:
+    """libclm runs the last layer's out_proj / LN2 / fc1 / fc2 on the pooled rows only unless
+    $CLM_NO_PRUNE=1 (capi.cpp run_layers); the FLOP / byte counts below follow it."""
+    return os.environ.get("CLM_NO_PRUNE", "0") in ("", "0")
+
+
+def flops_per_pair(cfg, pruned=None) -> dict:
     """Algorithmic FLOPs per image / caption (2 x MAC of every GEMM + full-T^2 attention,
-    LoRA unmerged), SURVEY §8(d)."""
-    def tower(d, L, mlp, T, lora_w):
-        per_layer = 2 * T * d * (3 * d + d + 2 * mlp) + 4 * T * T * d + lora_w * T
-        return L * per_layer
+    LoRA unmerged), SURVEY §8(d). With the last layer pruned, its out_proj / fc1 / fc2 (and
+    their LoRA) count one pooled row instead of T."""
+    pruned = pruned_last_layer() if pruned is None else pruned
     r = cfg.lora_r
 
-    def lora_tok(d, mlp):   # per token and layer: x.A^T (r x fin) + (.)B^T (fout x r) per target
+    def lora_tok(d, mlp, targets):   # per token and layer: x.A^T (r x fin) + (.)B^T (fout x r)
         dims = {"q_proj": (d, d), "k_proj": (d, d), "v_proj": (d, d), "out_proj": (d, d),
                 "fc1": (d, mlp), "fc2": (mlp, d)}
-        return sum(2 * r * (dims[t][0] + dims[t][1]) for t in cfg.lora_targets if t in dims)
+        return sum(2 * r * (dims[t][0] + dims[t][1]) for t in cfg.lora_targets if t in dims and t in targets)
+
+    def tower(d, L, mlp, T):
+        qkv = ("q_proj", "k_proj", "v_proj")
+        rest = ("out_proj", "fc1", "fc2")
+        front = 2 * T * d * 3 * d + 4 * T * T * d + lora_tok(d, mlp, qkv) * T   # q/k/v + attention
+        back = 2 * d * (d + 2 * mlp) + lora_tok(d, mlp, rest)                     # per row
+        return L * front + (L - 1) * T * back + (1 if pruned else T) * back
     v, t = cfg.vision, cfg.text
     P = cfg.num_patches
-    img = tower(v.hidden, v.layers, v.mlp, P + 1, lora_tok(v.hidden, v.mlp)) \
+    img = tower(v.hidden, v.layers, v.mlp, P + 1) \
         + 2 * P * (cfg.channels * cfg.patch ** 2) * v.hidden + 2 * v.hidden * cfg.proj_dim
-    txt = tower(t.hidden, t.layers, t.mlp, cfg.max_pos, lora_tok(t.hidden, t.mlp)) + 2 * t.hidden * cfg.proj_dim
+    txt = tower(t.hidden, t.layers, t.mlp, cfg.max_pos) + 2 * t.hidden * cfg.proj_dim
     return {"image": float(img), "caption": float(txt)}
 
 
 def gemm_algorithmic_bytes(cfg, B) -> float:
     """Compulsory HBM bytes of one step's GEMMs: A read once, W read once, output written once
-    (fp32 residual read + written for out_proj / fc2), bf16 operands."""
+    (fp32 residual read + written for out_proj / fc2), bf16 operands; the pruned last layer's
+    out_proj / fc1 / fc2 on B rows."""
     tot = 0.0
     for tw, T in ((cfg.vision, cfg.vision_seq), (cfg.text, cfg.max_pos)):
-        M, d, f = B * T, tw.hidden, tw.mlp
-        per_layer = (M * d * 2 + 3 * d * d * 2 + M * 3 * d * 2        # qkv
-                     + M * d * 2 + d * d * 2 + M * d * 8               # out (+ fp32 residual RMW)
-                     + M * d * 2 + f * d * 2 + M * f * 2               # fc1
-                     + M * f * 2 + d * f * 2 + M * d * 8)              # fc2 (+ residual RMW)
-        tot += tw.layers * per_layer
+        d, f = tw.hidden, tw.mlp
+
+        def front(M):
+            return M * d * 2 + 3 * d * d * 2 + M * 3 * d * 2                    # qkv
+
+        def back(M):
+            return (M * d * 2 + d * d * 2 + M * d * 8                            # out (+ fp32 residual RMW)
+                    + M * d * 2 + f * d * 2 + M * f * 2                          # fc1
+                    + M * f * 2 + d * f * 2 + M * d * 8)                         # fc2 (+ residual RMW)
+        M = B * T
+        tot += tw.layers * front(M) + (tw.layers - 1) * back(M) + back(B if pruned_last_layer() else M)
     P = B * cfg.num_patches
     tot += P * cfg.channels * cfg.patch ** 2 * 2 + cfg.vision.hidden * cfg.channels * cfg.patch ** 2 * 2 + \
         B * cfg.vision_seq * cfg.vision.hidden * 4

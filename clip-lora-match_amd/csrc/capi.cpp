@@ -124,6 +124,8 @@ struct Tower {
   float* h = nullptr;
   u16 *X = nullptr, *QKV = nullptr, *O = nullptr, *Hm = nullptr, *P = nullptr;
   float* pooled = nullptr;  // [max_batch, proj_dim] un-normalised projections
+  float* hc = nullptr;      // [max_batch, d] pooled residual rows of the pruned last layer
+  u16* Oc = nullptr;        // [max_batch, ldo] their attention-output rows
   int64_t ldx = 0, ldo = 0, ldm = 0;
 };
 
@@ -427,6 +429,8 @@ int build_tower(clm_ctx* c, Tower& T, bool vision) {
   if ((r = c->dalloc(&T.O, (size_t)T.maxM * T.ldo))) return r;
   if ((r = c->dalloc(&T.Hm, (size_t)T.maxM * T.ldm))) return r;
   if ((r = c->dalloc(&T.pooled, (size_t)B * d.proj_dim))) return r;
+  if ((r = c->dalloc(&T.hc, (size_t)B * T.d))) return r;
+  if ((r = c->dalloc(&T.Oc, (size_t)B * T.ldo))) return r;
   return CLM_OK;
 }
 
@@ -474,35 +478,66 @@ struct ProfScope {
   } while (0)
 
 // LN into X for a layer's q/k/v GEMM input (A_qkv extension in unmerged mode)
-LnArgs ln_into_x(clm_ctx* c, Tower& T, int64_t M, const float* g, const float* b, const float* loraA, int r_ext) {
+LnArgs ln_into_x(clm_ctx* c, Tower& T, int64_t M, const float* g, const float* b, const float* loraA, int r_ext,
+                 float* h = nullptr) {
   LnArgs a{};
-  a.mode = 0; a.src = T.h; a.lds = T.d; a.hf = T.h; a.ldh = T.d;
+  if (!h) h = T.h;
+  a.mode = 0; a.src = h; a.lds = T.d; a.hf = h; a.ldh = T.d;
   a.g1 = g; a.b1 = b; a.y = T.X; a.ldy = T.ldx;
   a.loraA = loraA; a.r_ext = r_ext; a.r_pad = loraA ? RPAD : 0;
   a.M = (int)M; a.d = T.d; a.eps = c->desc.ln_eps;
   return a;
 }
 
-// encoder layers on the residual stream T.h; the first layer's LN1 output must already be in T.X
-int run_layers(clm_ctx* c, Tower& T, int B, int S, bool causal, hipStream_t st) {
+// Last-layer pruning (default; $CLM_NO_PRUNE=1 runs every row): the encoders return only the
+// pooled row of each item (vision CLS row 0, text first-EOS row: TF/models/clip/
+// modeling_clip.py:558-580, 650), and after the last layer's attention every op is row-wise
+// (out_proj, LN2, fc1, fc2 + their LoRA). So the last layer runs q/k/v and attention on all
+// B*S rows, then out_proj .. fc2 on the B pooled rows only (gathered into T.hc / T.Oc): the
+// pooled embeddings are the same rows through the same kernels.
+bool prune_last_layer() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("CLM_NO_PRUNE");
+    v = (e && atoi(e)) ? 0 : 1;
+  }
+  return v == 1 && !(g_gemm_debug & 8);   // clm_debug_set bit 8: every row (tests)
+}
+
+// encoder layers on the residual stream T.h; the first layer's LN1 output must already be in T.X.
+// Returns with the pooled rows in T.hc (pruned: *pooled_rows = true) or all rows in T.h.
+int run_layers(clm_ctx* c, Tower& T, int B, int S, bool causal, const int32_t* ids, bool* pooled_rows,
+               hipStream_t st) {
   const bool bf = c->bf16();
-  const int64_t M = (int64_t)B * S;
+  const bool prune = prune_last_layer();
+  *pooled_rows = false;
   for (int l = 0; l < T.L; ++l) {
     LayerW& Lw = T.layers[l];
+    int64_t M = (int64_t)B * S;
     GemmArgs g{};
     g.A = T.X; g.lda = T.ldx; g.W = Lw.w_qkv; g.ldw = Lw.k_qkv; g.M = (int)M; g.N = 3 * T.d; g.K = Lw.k_qkv;
     g.out = T.QKV; g.ldo = 3 * T.d; g.bias = Lw.b_qkv;
     { PROF(CLM_PROF_GEMM, 2.0 * M * g.N * g.K); KCHK(gemm(bf, EPI_STORE, g, st)); }
     { PROF(CLM_PROF_ATTN, 4.0 * B * T.H * (double)S * S * 64);
       KCHK(attention(bf, causal, T.QKV, 3 * T.d, T.O, T.ldo, B, S, T.H, T.d, st)); }
+    float* h = T.h;
+    u16* O = T.O;
+    if (prune && l + 1 == T.L) {
+      { PROF(CLM_PROF_OTHER, (double)B * T.d * 6.0);
+        KCHK(gather_pooled(T.h, T.d, T.O, T.ldo, B, S, T.d, ids, c->desc.eos_token_id, T.hc, T.Oc, T.ldo, st)); }
+      M = B;
+      h = T.hc;
+      O = T.Oc;
+      *pooled_rows = true;
+    }
     if (Lw.r_out) { PROF(CLM_PROF_OTHER, 2.0 * M * T.d + 4.0 * Lw.r_out * T.d);
-      KCHK(lora_down(bf, T.O, T.ldo, (int)M, T.d, Lw.a_out, Lw.r_out, RPAD, st)); }
+      KCHK(lora_down(bf, O, T.ldo, (int)M, T.d, Lw.a_out, Lw.r_out, RPAD, st)); }
     g = GemmArgs{};
-    g.A = T.O; g.lda = T.ldo; g.W = Lw.w_out; g.ldw = Lw.k_out; g.M = (int)M; g.N = T.d; g.K = Lw.k_out;
-    g.out = T.h; g.ldo = T.d; g.bias = Lw.b_out;
+    g.A = O; g.lda = T.ldo; g.W = Lw.w_out; g.ldw = Lw.k_out; g.M = (int)M; g.N = T.d; g.K = Lw.k_out;
+    g.out = h; g.ldo = T.d; g.bias = Lw.b_out;
     { PROF(CLM_PROF_GEMM, 2.0 * M * g.N * g.K); KCHK(gemm(bf, EPI_RESID, g, st)); }
     { PROF(CLM_PROF_LN, (double)M * T.d * 6.0);
-      KCHK(layernorm(bf, ln_into_x(c, T, M, Lw.ln2_g, Lw.ln2_b, Lw.a_fc1, Lw.r_fc1), st)); }
+      KCHK(layernorm(bf, ln_into_x(c, T, M, Lw.ln2_g, Lw.ln2_b, Lw.a_fc1, Lw.r_fc1, h), st)); }
     g = GemmArgs{};
     g.A = T.X; g.lda = T.ldx; g.W = Lw.w_fc1; g.ldw = Lw.k_fc1; g.M = (int)M; g.N = T.mlp; g.K = Lw.k_fc1;
     g.out = T.Hm; g.ldo = T.ldm; g.bias = Lw.b_fc1;
@@ -511,7 +546,7 @@ int run_layers(clm_ctx* c, Tower& T, int B, int S, bool causal, hipStream_t st) 
       KCHK(lora_down(bf, T.Hm, T.ldm, (int)M, T.mlp, Lw.a_fc2, Lw.r_fc2, RPAD, st)); }
     g = GemmArgs{};
     g.A = T.Hm; g.lda = T.ldm; g.W = Lw.w_fc2; g.ldw = Lw.k_fc2; g.M = (int)M; g.N = T.d; g.K = Lw.k_fc2;
-    g.out = T.h; g.ldo = T.d; g.bias = Lw.b_fc2;
+    g.out = h; g.ldo = T.d; g.bias = Lw.b_fc2;
     { PROF(CLM_PROF_GEMM, 2.0 * M * g.N * g.K); KCHK(gemm(bf, EPI_RESID, g, st)); }
     if (l + 1 < T.L) {
       LayerW& Ln = T.layers[l + 1];
@@ -529,6 +564,8 @@ Tower ws_view(const Tower& T0, int b0, int rows, int patches, int proj_dim) {
   T.h += r0 * T.d; T.X += r0 * T.ldx; T.QKV += r0 * 3 * T.d; T.O += r0 * T.ldo; T.Hm += r0 * T.ldm;
   if (T.P) T.P += (int64_t)b0 * patches * T.kp;
   T.pooled += (int64_t)b0 * proj_dim;
+  T.hc += (int64_t)b0 * T.d;
+  T.Oc += (int64_t)b0 * T.ldo;
   return T;
 }
 
@@ -547,10 +584,11 @@ int encode_image_chunk(clm_ctx* c, Tower& T, const void* pix, int layout, int B,
   LnArgs a = ln_into_x(c, T, (int64_t)B * Tn, T.pre_g, T.pre_b, T.layers[0].a_qkv, T.layers[0].r_qkv);
   a.g2 = T.layers[0].ln1_g; a.b2 = T.layers[0].ln1_b;  // pre_layrnorm (in place) then layer-0 LN1
   { PROF(CLM_PROF_LN, (double)B * Tn * T.d * 10.0); KCHK(layernorm(bf, a, st)); }
-  int r = run_layers(c, T, B, Tn, false, st);
+  bool pooled_rows = false;
+  int r = run_layers(c, T, B, Tn, false, nullptr, &pooled_rows, st);
   if (r) return r;
   { PROF(CLM_PROF_OTHER, (double)B * (T.d * 4.0 + d.proj_dim * 4.0) + (double)T.d * d.proj_dim * 4.0);
-    KCHK(pool_project(T.h, T.d, B, Tn, T.d, nullptr, d.eos_token_id, T.fin_g, T.fin_b, d.ln_eps, T.projT,
+    KCHK(pool_project(pooled_rows ? T.hc : T.h, T.d, B, pooled_rows ? 1 : Tn, T.d, nullptr, d.eos_token_id, T.fin_g, T.fin_b, d.ln_eps, T.projT,
                       d.proj_dim, T.pooled, out, out_dtype == CLM_F32 ? 0 : 1, normalize, st)); }
   return CLM_OK;
 }
@@ -565,10 +603,12 @@ int encode_text_chunk(clm_ctx* c, Tower& T, const int32_t* ids_dev, int B, int L
   a.y = T.X; a.ldy = T.ldx; a.loraA = T.layers[0].a_qkv; a.r_ext = T.layers[0].r_qkv;
   a.r_pad = a.loraA ? RPAD : 0; a.M = B * L; a.d = T.d; a.eps = d.ln_eps;
   { PROF(CLM_PROF_LN, (double)B * L * T.d * 14.0); KCHK(layernorm(bf, a, st)); }
-  int r = run_layers(c, T, B, L, true, st);
+  bool pooled_rows = false;
+  int r = run_layers(c, T, B, L, true, ids_dev, &pooled_rows, st);
   if (r) return r;
   { PROF(CLM_PROF_OTHER, (double)B * (T.d * 4.0 + d.proj_dim * 4.0 + L * 4.0) + (double)T.d * d.proj_dim * 4.0);
-    KCHK(pool_project(T.h, T.d, B, L, T.d, ids_dev, d.eos_token_id, T.fin_g, T.fin_b, d.ln_eps, T.projT,
+    KCHK(pool_project(pooled_rows ? T.hc : T.h, T.d, B, pooled_rows ? 1 : L, T.d, pooled_rows ? nullptr : ids_dev,
+                      d.eos_token_id, T.fin_g, T.fin_b, d.ln_eps, T.projT,
                       d.proj_dim, T.pooled, out, out_dtype == CLM_F32 ? 0 : 1, normalize, st)); }
   return CLM_OK;
 }

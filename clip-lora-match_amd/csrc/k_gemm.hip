@@ -115,16 +115,19 @@ __global__ __launch_bounds__(WM * WN * 64, (Cfg<BM, BN, WM, WN, STAGES>::WAVES_P
     if (s < S) stage_next(s);
 
   // stores a tile end leaves in flight (the ragged scalar path stores in branches: none counted)
-  constexpr int E = epi_min_stores<EPI, C::TM, C::TN>();
+  constexpr int E0 = epi_min_stores<EPI, C::TM, C::TN>();
+  constexpr int E = E0 + C::L * (STAGES - 2) > 63 ? 63 - C::L * (STAGES - 2) : E0;   // 6-bit vmcnt: over-wait
   const bool vec_epi = (g.N % 4) == 0 && (g.ldo % 4) == 0 && !(g.debug & 1);
   int c_i = 0, c_kt = 0, m0, n0;
   coords(0, m0, n0);
-  bool prev_end = false;
+  int since_end = STAGES;   // K-steps since the last tile end
   for (int s = 0; s < S; ++s) {
     // retire K-step s's DMA, leaving younger ones in flight: the STAGES-2 later K-steps' DMA
-    // and, right after a tile end, that epilogue's stores (issued after this DMA)
+    // and, for STAGES-1 steps after a tile end, that epilogue's stores (the DMA of those steps
+    // was issued before the stores; the first DMA issued after them is waited STAGES steps on)
     const bool more = s + STAGES - 2 < S;
-    const bool pe = prev_end && vec_epi;
+    ++since_end;
+    const bool pe = vec_epi && since_end <= STAGES - 1;
     if (more) {
       if (pe) wait_vmcnt<C::L * (STAGES - 2) + E>();
       else wait_vmcnt<C::L * (STAGES - 2)>();
@@ -155,8 +158,8 @@ __global__ __launch_bounds__(WM * WN * 64, (Cfg<BM, BN, WM, WN, STAGES>::WAVES_P
 #pragma unroll
         for (int nb = 0; nb < C::TN; ++nb) acc[mb][nb] = mfma16<BF>(bw[nb], af[mb], acc[mb][nb]);
     }
-    prev_end = ++c_kt == nk;
-    if (prev_end) {
+    if (++c_kt == nk) {
+      since_end = 0;
       if (g.debug & 1) {   // timing diagnostic: main loop only
 #pragma unroll
         for (int mb = 0; mb < C::TM; ++mb)

@@ -180,7 +180,11 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void gemm2_kernel(GemmArgs g) {
           if (stored) { if (more) wait_vmcnt<L * (NS - 2) + 1>(); else wait_vmcnt<1>(); }
           else { if (more) wait_vmcnt<L * (NS - 2)>(); else wait_vmcnt<0>(); }
         } else {
-          if (kt == 0 && ti > 0 && vec_epi) { if (more) wait_vmcnt<L * (NS - 2) + E>(); else wait_vmcnt<E>(); }
+          // the previous tile's E epilogue stores were issued after DMA(s+NS-1) of its last step:
+          // with NS = 3 they sit between DMA(s+1) and DMA(s+2) at kt = 1 too, so they need not
+          // drain until kt = 2 -- three K-steps for the burst instead of one
+          if (kt == 0 && ti > 0 && vec_epi) { if (more) wait_vmcnt<(L * (NS - 2) + E > 63 ? 63 : L * (NS - 2) + E)>(); else wait_vmcnt<E>(); }
+          else if (NS == 3 && kt == 1 && ti > 0 && vec_epi) { if (more) wait_vmcnt<(L + E > 63 ? 63 : L + E)>(); else wait_vmcnt<E>(); }
           else { if (more) wait_vmcnt<L * (NS - 2)>(); else wait_vmcnt<0>(); }
         }
         lds_barrier();

@@ -348,6 +348,42 @@ __global__ void write_cls_kernel(float* h, int64_t ldh, int B, int T, int d, con
 
 // ------------------------------------------------------- pool + projection --
 
+// The pooled row of item b: 0 (vision CLS), or with ids the first EOS token (argmax(ids) for
+// the legacy eos_token_id == 2 rule) -- CLIPTextTransformer's pooling
+// (TF/models/clip/modeling_clip.py:558-580; vision CLS: :650). Whole wave, uniform result.
+__device__ __forceinline__ int pooled_row(const int32_t* ids, int b, int T, int eos, int lane) {
+  if (!ids) return 0;
+  const int32_t* id = ids + (int64_t)b * T;
+  int best = INT_MAX, bestv = INT_MIN;
+  for (int t = lane; t < T; t += 64) {
+    const int v = id[t];
+    if (eos == 2) { if (v > bestv) { bestv = v; best = t; } }
+    else if (v == eos && t < best) best = t;
+  }
+  if (eos == 2) {
+    for (int o = 32; o > 0; o >>= 1) {
+      const int ov = __shfl_xor(bestv, o, 64), ob = __shfl_xor(best, o, 64);
+      if (ov > bestv || (ov == bestv && ob < best)) { bestv = ov; best = ob; }
+    }
+  } else {
+    for (int o = 32; o > 0; o >>= 1) best = min(best, __shfl_xor(best, o, 64));
+  }
+  return best == INT_MAX ? 0 : best;   // (ids == eos).argmax() is 0 when absent
+}
+
+// Last-layer pruning: one wave per item copies its pooled row of the residual stream h and of
+// the attention output O into the compact hc [B][d] / Oc [B][ldoc] (see run_layers).
+__global__ __launch_bounds__(64) void gather_pooled_kernel(const float* h, int64_t ldh, const u16* O, int64_t ldo,
+                                                           int T, int d, const int32_t* ids, int eos, float* hc,
+                                                           u16* Oc, int64_t ldoc) {
+  const int b = blockIdx.x, lane = threadIdx.x;
+  const int64_t row = (int64_t)b * T + pooled_row(ids, b, T, eos, lane);
+  for (int e = lane * 4; e < d; e += 256) {
+    *(float4*)(hc + (int64_t)b * d + e) = *(const float4*)(h + row * ldh + e);
+    *(u32x2*)(Oc + (int64_t)b * ldoc + e) = *(const u32x2*)(O + row * ldo + e);
+  }
+}
+
 // Grid (B/PRB row blocks) x (D/64 column blocks). Each block LayerNorms its PRB
 // pooled rows into LDS (layout [i][row]: one ds_read_b128 = 4 rows of element i),
 // then thread (c, part) accumulates column c over a quarter of d for all PRB rows
@@ -374,25 +410,7 @@ __global__ __launch_bounds__(256) void pool_project_kernel(const float* h, int64
       for (int e = lane; e < d; e += 64) y[e * PRB + rr] = 0.f;
       continue;
     }
-    int prow = 0;
-    if (ids) {  // first EOS (or argmax(ids) for the legacy eos_token_id == 2 rule)
-      const int32_t* id = ids + (int64_t)b * T;
-      int best = INT_MAX, bestv = INT_MIN;
-      for (int t = lane; t < T; t += 64) {
-        const int v = id[t];
-        if (eos == 2) { if (v > bestv) { bestv = v; best = t; } }
-        else if (v == eos && t < best) best = t;
-      }
-      if (eos == 2) {
-        for (int o = 32; o > 0; o >>= 1) {
-          const int ov = __shfl_xor(bestv, o, 64), ob = __shfl_xor(best, o, 64);
-          if (ov > bestv || (ov == bestv && ob < best)) { bestv = ov; best = ob; }
-        }
-      } else {
-        for (int o = 32; o > 0; o >>= 1) best = min(best, __shfl_xor(best, o, 64));
-      }
-      prow = best == INT_MAX ? 0 : best;   // (ids == eos).argmax() is 0 when absent
-    }
+    const int prow = pooled_row(ids, b, T, eos, lane);
     const float* x = h + ((int64_t)b * T + prow) * ldh;
     float s = 0.f;
     for (int e = lane; e < d; e += 64) s += x[e];
@@ -545,6 +563,14 @@ hipError_t write_cls(float* h, int64_t ldh, int B, int T, int d, const float* cl
                      hipStream_t s) {
   if (B <= 0) return hipSuccess;
   write_cls_kernel<<<B, 256, 0, s>>>(h, ldh, B, T, d, cls, pos);
+  return hipGetLastError();
+}
+
+hipError_t gather_pooled(const float* h, int64_t ldh, const u16* O, int64_t ldo, int B, int T, int d,
+                         const int32_t* ids, int eos, float* hc, u16* Oc, int64_t ldoc, hipStream_t s) {
+  if (B <= 0) return hipSuccess;
+  if ((d % 4) || (ldh % 4) || (ldo % 4) || (ldoc % 4)) return hipErrorInvalidValue;
+  gather_pooled_kernel<<<B, 64, 0, s>>>(h, ldh, O, ldo, T, d, ids, eos, hc, Oc, ldoc);
   return hipGetLastError();
 }
 

@@ -74,6 +74,10 @@ hipError_t write_cls(float* h, int64_t ldh, int B, int T, int d, const float* cl
 // pooled row -> LN -> projection (fp32, projT [d, D]) -> optional L2 norm -> out
 //   ids == null: row b*T (CLS); else row b*T + (first eos in ids[b]) (argmax if eos==2)
 //   tmp: [B, D] fp32 workspace
+// Last-layer pruning: hc[b] = h[b*T + prow_b], Oc[b][:d] = O[b*T + prow_b][:d], prow_b the
+// pooled row (0, or the first EOS of ids).
+hipError_t gather_pooled(const float* h, int64_t ldh, const u16* O, int64_t ldo, int B, int T, int d,
+                         const int32_t* ids, int eos, float* hc, u16* Oc, int64_t ldoc, hipStream_t s);
 hipError_t pool_project(const float* h, int64_t ldh, int B, int T, int d, const int32_t* ids,
                         int eos, const float* g, const float* bta, float eps, const float* projT,
                         int D, float* tmp, void* out, int out_dtype, int normalize, hipStream_t s);

@@ -163,9 +163,11 @@ int clm_gemm(int hip_device, int dtype, int epilogue, int config, const void* A,
              const void* W, int64_t ldw, int M, int N, int K, void* out, int64_t ldo,
              const float* bias, const float* rscale, const float* cscale, void* stream);
 int clm_gemm_num_configs(void);
-/* diagnostic flags for later clm_gemm calls (micro-benchmarks only; 0 in production):
- * bit 0 = skip the epilogue (accumulators kept live), bit 1 = run the epilogue but drop
- * every store. Initialised from $CLM_GEMM_DEBUG. */
+/* diagnostic flags (micro-benchmarks and tests only; 0 in production), initialised from
+ * $CLM_GEMM_DEBUG: for later clm_gemm calls bit 0 = skip the epilogue (accumulators kept
+ * live), bit 1 = run the epilogue but drop every store, bit 2 = one tile per workgroup
+ * instead of the persistent grid; for later encodes bit 3 (value 8) = run the last encoder
+ * layer on every row instead of only the pooled rows (same embeddings, for parity tests). */
 void clm_debug_set(int flags);
 /* attention over qkv [B*T, 3*H*64] (q pre-scaled), out [B*T, ldo] (device pointers) */
 int clm_attention(int hip_device, int dtype, int causal, const void* qkv, void* out, int64_t ldo,

@@ -186,3 +186,25 @@ def test_encode_pair_matches_separate(graph, split):
     assert torch.equal(oi, m.encode_pixels(imgs))
     with pytest.raises(ValueError):
         m.encode_pair(imgs.cpu(), ids)
+
+
+@pytest.mark.parametrize("preset,mode", [("tiny", "merged"), ("tiny", "unmerged"), ("ViT-B/32", "merged"),
+                                         ("ViT-B/32", "unmerged")])
+def test_last_layer_pruning_exact(preset, mode):
+    """The last layer's out_proj / LN2 / fc1 / fc2 run on the pooled rows only (capi.cpp
+    run_layers): embeddings must equal the every-row run (clm_debug_set bit 8), with first-EOS
+    pooling over ragged caption lengths and a caption without EOS (pools row 0)."""
+    from clip_lora_match_amd import _capi as C
+    m, cfg, sd, lora = _model(preset, "bfloat16", mode, max_batch=40)
+    imgs = torch.from_numpy(syn.images_u8(37, cfg.image_size, 11)).cuda()
+    ids = syn.captions(37, cfg.max_pos, cfg.bos_token_id, cfg.eos_token_id, 12)
+    ids[5] = np.arange(cfg.max_pos) + 5   # no EOS at all
+    outs = {}
+    try:
+        for flag in (0, 8):
+            C.lib().clm_debug_set(flag)
+            outs[flag] = (m.encode_pixels(imgs).cpu().numpy(), m.encode_ids(torch.from_numpy(ids).cuda()).cpu().numpy())
+    finally:
+        C.lib().clm_debug_set(0)
+    for a, b in zip(outs[0], outs[8]):
+        assert np.max(np.abs(a - b)) <= 1e-6, f"pruned vs every-row: {np.max(np.abs(a - b)):.3e}"

@@ -1,7 +1,7 @@
 """GEMM probe: per encoder shape, time (a) torch.mm bf16 (hipBLASLt) as a same-box reference,
 (b) clm_gemm per tile config with the real epilogue, (c) main loop only (debug bit 1),
 (d) epilogue computed but every store dropped (debug bit 2), (e) K = 64 (fixed cost),
-(f) one tile per workgroup instead of the persistent grid (debug bit 4).
+(f) one tile per workgroup instead of the persistent grid (debug bit 4), (g) no bias vector.
 All variants of one shape run interleaved in ONE process (median of rounds), random operands.
 usage: python tools/gemm_probe.py [cfg,cfg,...] [shape,shape,...] -> one JSON line per (shape, variant)"""
 import json
@@ -48,11 +48,11 @@ for name in only:
     ob = torch.empty((M, N), device=dev, dtype=torch.bfloat16)
     out2 = torch.zeros_like(out)
 
-    def ours(cfg, dbg, k=K):
+    def ours(cfg, dbg, k=K, use_bias=True):
         def f():
             L.clm_debug_set(dbg)
             C.check(L.clm_gemm(0, C.CLM_BF16, epi, cfg, C.ptr(A), K, C.ptr(W), K, M, N, k, C.ptr(out), N,
-                               C.ptr(bias), None, None, sptr))
+                               C.ptr(bias) if use_bias else None, None, None, sptr))
         return f
 
     variants = {"blas": lambda: torch.mm(A, W.t(), out=ob), "fill_out": lambda: out.fill_(1.0),
@@ -62,9 +62,15 @@ for name in only:
         variants[f"c{cfg}_np"] = ours(cfg, 4)
         variants[f"c{cfg}_noepi"] = ours(cfg, 1)
         variants[f"c{cfg}_nostore"] = ours(cfg, 2)
+        variants[f"c{cfg}_nobias"] = ours(cfg, 0, K, False)
         variants[f"c{cfg}_k64"] = ours(cfg, 0, 64)
+        variants[f"c{cfg}_k64nobias"] = ours(cfg, 0, 64, False)
         variants[f"c{cfg}_k64noepi"] = ours(cfg, 1, 64)
         variants[f"c{cfg}_k64nostore"] = ours(cfg, 2, 64)
+    keep = os.environ.get("PROBE_VARIANTS")   # e.g. "blas,full": suffixes to keep
+    if keep:
+        ks = keep.split(",")
+        variants = {k: v for k, v in variants.items() if k in ks or k.split("_", 1)[-1] in ks}
     for fn in variants.values():
         fn()
     torch.cuda.synchronize()
