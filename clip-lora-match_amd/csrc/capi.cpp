@@ -1398,4 +1398,31 @@ int clm_l2_normalize(int hip_device, float* rows, int64_t n, int dim, void* stre
   return CLM_OK;
 }
 
+int clm_fuse_queries(int hip_device, const float* a, float w_a, const float* b, float w_b, int64_t n,
+                     int dim, float* out, void* stream) {
+  if (n < 0 || dim <= 0 || (n > 0 && (!a || !out))) return fail(CLM_E_ARG, "bad argument");
+  if (n == 0) return CLM_OK;
+  DeviceGuard g(hip_device);
+  hipStream_t st = (hipStream_t)stream;
+  const bool dev = is_device_ptr(a);
+  if (dev != is_device_ptr(out) || (b && dev != is_device_ptr(b)))
+    return fail(CLM_E_ARG, "fuse_queries: a, b and out must all be device or all host pointers");
+  if (dev) {
+    KCHK(fuse_rows(a, w_a, b, w_b, n, dim, out, st));
+    return CLM_OK;
+  }
+  const size_t bytes = (size_t)n * dim * 4;
+  float* t = nullptr;
+  if (hipMalloc(&t, bytes * (b ? 2 : 1)) != hipSuccess) { (void)hipGetLastError(); return fail(CLM_E_OOM, "workspace"); }
+  float* tb = b ? t + (size_t)n * dim : nullptr;
+  hipError_t e = hipMemcpyAsync(t, a, bytes, hipMemcpyHostToDevice, st);
+  if (e == hipSuccess && b) e = hipMemcpyAsync(tb, b, bytes, hipMemcpyHostToDevice, st);
+  if (e == hipSuccess) e = fuse_rows(t, w_a, tb, w_b, n, dim, t, st);
+  if (e == hipSuccess) e = hipMemcpyAsync(out, t, bytes, hipMemcpyDeviceToHost, st);
+  if (e == hipSuccess) e = hipStreamSynchronize(st);
+  (void)hipFree(t);
+  if (e != hipSuccess) return fail(CLM_E_HIP, std::string("fuse_queries: ") + hipGetErrorString(e));
+  return CLM_OK;
+}
+
 }  // extern "C"

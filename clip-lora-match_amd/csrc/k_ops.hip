@@ -511,6 +511,29 @@ __global__ __launch_bounds__(256) void l2n_kernel(float* rows, int64_t n, int di
   for (int e = lane; e < dim; e += 64) r[e] = r[e] / nrm;
 }
 
+// Query fusion (SeekerService._build_query_embedding, seeker_service.py:148-157): one wave per
+// row, out = v / ||v|| with v = wa*a + wb*b (b == nullptr: v = a, the single-modality branch).
+// The weighted sum is rounded like the reference's (two products, then one add: no FMA contraction).
+__global__ __launch_bounds__(256) void fuse_rows_kernel(const float* a, float wa, const float* b, float wb,
+                                                         int64_t n, int dim, float* out) {
+  const int lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= n) return;
+  const float* ra = a + row * dim;
+  const float* rb = b ? b + row * dim : nullptr;
+  float* ro = out + row * dim;
+  float s = 0.f;
+  for (int e = lane; e < dim; e += 64) {
+    const float v = rb ? __fadd_rn(__fmul_rn(wa, ra[e]), __fmul_rn(wb, rb[e])) : ra[e];
+    s += v * v;
+  }
+  const float nrm = sqrtf(wave_sum(s));
+  for (int e = lane; e < dim; e += 64) {
+    const float v = rb ? __fadd_rn(__fmul_rn(wa, ra[e]), __fmul_rn(wb, rb[e])) : ra[e];
+    ro[e] = v / nrm;
+  }
+}
+
 __global__ __launch_bounds__(256) void f32_to_f16_kernel(const float* src, int64_t total, u16* dst) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
        i += (int64_t)gridDim.x * blockDim.x)
@@ -604,6 +627,13 @@ hipError_t sample_rows(const u16* rows, const float* inv, int64_t n, int dim, in
 hipError_t l2_normalize_rows(float* rows, int64_t n, int dim, hipStream_t s) {
   if (n <= 0) return hipSuccess;
   l2n_kernel<<<(unsigned)((n + 3) / 4), 256, 0, s>>>(rows, n, dim);
+  return hipGetLastError();
+}
+
+hipError_t fuse_rows(const float* a, float wa, const float* b, float wb, int64_t n, int dim, float* out,
+                     hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  fuse_rows_kernel<<<(unsigned)((n + 3) / 4), 256, 0, s>>>(a, wa, b, wb, n, dim, out);
   return hipGetLastError();
 }
 

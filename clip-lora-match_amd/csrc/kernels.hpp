@@ -100,6 +100,8 @@ hipError_t topk_rows(const float* scores, int64_t lds, int64_t nq, int64_t C, in
 hipError_t topk_merge(const float* in_s, const int64_t* in_i, int64_t nq, int parts, int k_in,
                       int k, float* out_s, int64_t* out_i, hipStream_t s);
 hipError_t l2_normalize_rows(float* rows, int64_t n, int dim, hipStream_t s);
+hipError_t fuse_rows(const float* a, float wa, const float* b, float wb, int64_t n, int dim, float* out,
+                     hipStream_t s);
 // strided row sample: out[s] = rows[s * n / S] (fp16 rows + fp32 inverse norms)
 hipError_t sample_rows(const u16* rows, const float* inv, int64_t n, int dim, int64_t S, u16* out_rows,
                        float* out_inv, hipStream_t s);

@@ -1,0 +1,88 @@
+"""Index build: scripts/rebuild_index.py:28-115 on the gfx950 encode path, batched and
+optionally sharded over the GPUs of one node.
+
+The reference encodes each item's description one at a time (:64-77: encode_text, then
+a second `/ norm`), concatenates the rows and writes
+{"embeddings": [N, D] f32, "image_paths": [...], "texts": [...]} with torch.save (:86-93).
+Here one call encodes `batch_size` captions (or images) per launch sequence, the rows
+stay on the device until the save, and under torch.distributed each rank encodes its
+shard_range of the items and one all_gather assembles the index in item order
+(distributed.build_index_sharded). The file format is the reference's, so
+TextSearchIndex (ours or the reference's) loads it unchanged.
+
+The database query (:46-52) is the caller's: pass the items' descriptions / image paths.
+"""
+from __future__ import annotations
+
+from pathlib import Path
+from typing import Optional, Sequence, Union
+
+import torch
+import torch.distributed as dist
+
+from . import _capi as C
+
+
+def _renormalize(rows: torch.Tensor) -> torch.Tensor:
+    """The reference's second `text_emb / text_emb.norm(...)` (rebuild_index.py:72), on the device."""
+    rows = rows.float().contiguous()
+    if rows.shape[0]:
+        C.check(C.lib().clm_l2_normalize(rows.device.index, C.ptr(rows), rows.shape[0], rows.shape[1],
+                                         C.stream_of(rows.device)), "clm_l2_normalize")
+    return rows
+
+
+def encode_items(model, processor, texts: Optional[Sequence] = None, images: Optional[Sequence] = None,
+                 batch_size: int = 256, group=None) -> torch.Tensor:
+    """[N, D] f32 unit rows on the model's device, in item order, for N captions (str or token ids)
+    or N images (paths / arrays). Sharded over the ranks of `group` when torch.distributed is up."""
+    if (texts is None) == (images is None):
+        raise ValueError("pass exactly one of texts / images")
+    items = list(texts if texts is not None else images)
+    n = len(items)
+    D = model.cfg.proj_dim
+
+    def encode_rows(start: int, stop: int) -> torch.Tensor:
+        if stop <= start:
+            return torch.empty((0, D), dtype=torch.float32, device=model.device)
+        chunk = items[start:stop]
+        if texts is not None:
+            ids = processor.token_ids(chunk)
+            out = model.encode_ids(ids.to(model.device), normalize=True)
+        else:
+            from .clip_model import _encode_images
+            out = _encode_images(chunk, model, processor, normalize=True)
+        return _renormalize(out)
+
+    if dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1:
+        from .distributed import build_index_sharded
+        return build_index_sharded(encode_rows, n, batch_size, group)
+    outs = [encode_rows(s, min(s + batch_size, n)) for s in range(0, n, batch_size)]
+    return torch.cat(outs, 0) if outs else encode_rows(0, 0)
+
+
+def rebuild_index(model, processor, descriptions: Sequence, image_paths: Sequence[str],
+                  index_path: Union[str, Path], batch_size: int = 256, from_images: bool = False,
+                  group=None) -> torch.Tensor:
+    """rebuild_index.py:28-115: embed every item (its description by default, as the reference
+    does; its image with from_images=True), save the .pt index, return the [N, D] CPU rows.
+    Under torch.distributed only rank 0 writes the file. No items: nothing is written (:54-56)."""
+    if len(descriptions) != len(image_paths):
+        raise ValueError(f"{len(descriptions)} descriptions vs {len(image_paths)} image paths")
+    if len(descriptions) == 0:
+        return torch.empty((0, model.cfg.proj_dim), dtype=torch.float32)
+    if from_images:
+        rows = encode_items(model, processor, images=list(image_paths), batch_size=batch_size, group=group)
+    else:
+        rows = encode_items(model, processor, texts=list(descriptions), batch_size=batch_size, group=group)
+    rows = rows.cpu()
+    rank0 = not (dist.is_available() and dist.is_initialized()) or dist.get_rank(group) == 0
+    if rank0:
+        index_path = Path(index_path)
+        index_path.parent.mkdir(parents=True, exist_ok=True)
+        texts = [d if isinstance(d, str) else "" for d in descriptions]
+        torch.save({"embeddings": rows, "image_paths": [str(p) for p in image_paths], "texts": texts}, index_path)
+    return rows
+
+
+__all__ = ["encode_items", "rebuild_index"]

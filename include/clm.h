@@ -155,6 +155,12 @@ int clm_topk_merge(int hip_device, const float* scores, const int64_t* idx, int6
 /* rows [n, dim] f32 in place (device or host) */
 int clm_l2_normalize(int hip_device, float* rows, int64_t n, int dim, void* stream);
 
+/* query fusion, replaces SeekerService._build_query_embedding (src/embedding/seeker_service.py:84-157):
+ * out[i] = v / ||v|| with v = w_a*a[i] + w_b*b[i], rows [n, dim] f32; b == NULL gives out = a / ||a||
+ * (the single-modality branch, :149-152). a, b, out all device or all host; out may alias a. */
+int clm_fuse_queries(int hip_device, const float* a, float w_a, const float* b, float w_b, int64_t n,
+                     int dim, float* out, void* stream);
+
 /* Kernel-level entry points (unit tests and micro-benchmarks of the hot kernels).
  * clm_gemm: C[M,N] = A[M,K] . W[N,K]^T with dtype CLM_BF16|CLM_F16 operands (device
  * pointers), K % 64 == 0, epilogue CLM_EPI_*; config < 0 picks the tile heuristically. */

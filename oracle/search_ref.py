@@ -5,6 +5,9 @@ CPU restatement of the reference's cosine search:
   * search_with_embedding: query normalise :93, sims = q @ E^T :96,
     topk(min(k, N), largest, sorted) :98-99
   * similarity.cosine_similarity / top_k_similar    src/embedding/similarity.py:10-58
+  * SeekerService._build_query_embedding fusion      src/embedding/seeker_service.py:148-157
+    (restated only: the service module imports its DB / YOLO stack, so this
+    3-line rule is parity-unpinned by reference-produced vectors)
 with the tie rule the build defines (score desc, index asc) -- CPU torch.topk
 leaves exact ties unordered (SURVEY §7 hard part 2).
 
@@ -28,6 +31,20 @@ def cosine_scores(q: np.ndarray, E: np.ndarray, dtype=np.float64) -> np.ndarray:
     q = q / np.linalg.norm(q, axis=-1, keepdims=True)
     E = E / np.linalg.norm(E, axis=-1, keepdims=True)
     return q @ E.T
+
+
+def fuse_query(text_emb, image_emb, w_text: float = 0.5, w_image: float = 0.5) -> np.ndarray:
+    """seeker_service.py:148-157: one modality -> e / ||e||; both -> (w_t*t + w_i*i) / ||.||,
+    fp32 products and sum as torch evaluates `sum(w * e for e, w in embs)` (0 + w_t*t + w_i*i)."""
+    if text_emb is None and image_emb is None:
+        raise ValueError("need a text or an image embedding")
+    if text_emb is None or image_emb is None:
+        e = np.asarray(text_emb if text_emb is not None else image_emb, np.float32)
+        return (e / np.linalg.norm(e.astype(np.float64), axis=-1, keepdims=True)).astype(np.float32)
+    t = np.asarray(text_emb, np.float32)
+    i = np.asarray(image_emb, np.float32)
+    v = (np.float32(w_text) * t) + (np.float32(w_image) * i)
+    return (v / np.linalg.norm(v.astype(np.float64), axis=-1, keepdims=True)).astype(np.float32)
 
 
 def topk(scores: np.ndarray, k: int):

@@ -197,3 +197,101 @@ def test_filtered_path_overflow_falls_back():
     assert idx.stats()["overflow"] >= 1
     assert torch.equal(i[0], pos[:8])
     assert torch.all(s[0] > 0.999)
+
+
+# ---- query fusion (seeker_service.py:84-186) ------------------------------------------------
+def _unit_rows(n, d, seed):
+    x = np.random.default_rng(seed).standard_normal((n, d)).astype(np.float32)
+    return x / np.linalg.norm(x, axis=-1, keepdims=True)
+
+
+@pytest.mark.parametrize("n,d", [(1, 512), (300, 512), (7, 768), (5, 100)])
+def test_fuse_queries_vs_oracle(n, d):
+    from clip_lora_match_amd.seeker import fuse_query_embeddings
+    t, i = _unit_rows(n, d, 11), _unit_rows(n, d, 12)
+    for wt, wi in ((0.5, 0.5), (0.7, 0.3), (1.0, 0.0)):
+        got = fuse_query_embeddings(torch.from_numpy(t).cuda(), torch.from_numpy(i).cuda(), wt, wi)
+        assert got.device.type == "cuda" and got.shape == (n, d)
+        np.testing.assert_allclose(got.cpu().numpy(), S.fuse_query(t, i, wt, wi), atol=1e-6, rtol=0)
+    # single modality: renormalise that side (:149-152); either side
+    np.testing.assert_allclose(fuse_query_embeddings(None, torch.from_numpy(3 * i).cuda()).cpu().numpy(),
+                               S.fuse_query(None, 3 * i), atol=1e-6, rtol=0)
+    np.testing.assert_allclose(fuse_query_embeddings(torch.from_numpy(2 * t).cuda(), None).cpu().numpy(),
+                               S.fuse_query(2 * t, None), atol=1e-6, rtol=0)
+
+
+def test_fuse_queries_host_tensors_shapes_and_errors():
+    from clip_lora_match_amd.seeker import fuse_query_embeddings
+    t, i = _unit_rows(3, 512, 13), _unit_rows(3, 512, 14)
+    got = fuse_query_embeddings(torch.from_numpy(t[0]), torch.from_numpy(i[0]))   # host, (D,)
+    assert got.device.type == "cpu" and got.shape == (512,)
+    np.testing.assert_allclose(got.numpy(), S.fuse_query(t[0], i[0]), atol=1e-6, rtol=0)
+    with pytest.raises(ValueError):
+        fuse_query_embeddings(None, None)
+    with pytest.raises(ValueError):
+        fuse_query_embeddings(torch.from_numpy(t), torch.from_numpy(i[:2]))
+    # mixed residency: the host side is moved to the device; the result follows the text side
+    got = fuse_query_embeddings(torch.from_numpy(t).cuda(), torch.from_numpy(i))
+    np.testing.assert_allclose(got.cpu().numpy(), S.fuse_query(t, i), atol=1e-6, rtol=0)
+
+
+def test_fuse_queries_c_abi_host_pointers():
+    """clm_fuse_queries on host buffers (staged through HBM inside the library), in place,
+    and its argument checks."""
+    import ctypes
+
+    from clip_lora_match_amd import _capi as C
+    t, i = _unit_rows(9, 512, 15), _unit_rows(9, 512, 16)
+    out = np.empty_like(t)
+    vp = lambda a: ctypes.c_void_p(a.ctypes.data)  # noqa: E731
+    C.check(C.lib().clm_fuse_queries(0, vp(t), 0.6, vp(i), 0.4, 9, 512, vp(out), None))
+    np.testing.assert_allclose(out, S.fuse_query(t, i, 0.6, 0.4), atol=1e-6, rtol=0)
+    a = 5 * t.copy()
+    C.check(C.lib().clm_fuse_queries(0, vp(a), 1.0, None, 0.0, 9, 512, vp(a), None))   # in place, one side
+    np.testing.assert_allclose(a, S.fuse_query(5 * t, None), atol=1e-6, rtol=0)
+    assert C.lib().clm_fuse_queries(0, vp(t), 1.0, None, 0.0, 9, 0, vp(out), None) == C.CLM_E_ARG
+    assert C.lib().clm_fuse_queries(0, vp(t), 1.0, None, 0.0, 0, 512, vp(out), None) == C.CLM_OK
+    dev = torch.from_numpy(t).cuda()
+    with pytest.raises(ValueError):   # mixed device / host pointers are refused
+        C.check(C.lib().clm_fuse_queries(0, C.ptr(dev), 1.0, None, 0.0, 9, 512, vp(out), None))
+
+
+def test_build_query_embedding_and_search_items(tmp_path):
+    from PIL import Image
+
+    from conftest import synthetic as synth
+    from clip_lora_match_amd.engine import ClipLoraModel
+    from clip_lora_match_amd.processor import ClipProcessor
+    from clip_lora_match_amd.seeker import build_query_embedding, search_items
+    from oracle import clip_ref as R
+
+    cfg, sd, lora = synth("tiny")
+    m = ClipLoraModel(cfg, compute_dtype="float16", lora_mode="merged", max_batch=8)
+    m.load_tensors(sd)
+    m.load_tensors(lora)
+    m.finalize()
+    proc = ClipProcessor(cfg)
+    img = syn.images_u8(1, cfg.image_size, 21)
+    Image.fromarray(img[0]).save(tmp_path / "q.png")
+    ids = syn.captions(1, cfg.max_pos, cfg.bos_token_id, cfg.eos_token_id, 22)
+    row = [int(v) for v in ids[0]]
+    ri = R.image_features(sd, cfg, R.preprocess_u8(img, cfg.mean, cfg.std), lora)[0]
+    rt = R.text_features(sd, cfg, ids, lora)[0]
+    dev = m.device
+    both = build_query_embedding(row, tmp_path / "q.png", m, proc, dev)
+    assert both.device.type == "cpu" and both.dtype == torch.float32
+    ref = S.fuse_query(rt, ri)
+    assert 1 - float(np.dot(both.numpy(), ref)) <= 1e-5
+    only_img = build_query_embedding("   ", tmp_path / "q.png", m, proc, dev)   # blank text = absent (:98)
+    assert 1 - float(np.dot(only_img.numpy(), ri / np.linalg.norm(ri))) <= 1e-5
+    with pytest.raises(ValueError):
+        build_query_embedding("", None, m, proc, dev)
+    # resident index with the fused query planted at row 17: it must come back first
+    E = _unit_rows(64, cfg.proj_dim, 23)
+    E[17] = both.numpy()
+    index = TextSearchIndex(embeddings=torch.from_numpy(E), image_paths=[f"p{j}" for j in range(64)],
+                            texts=[f"t{j}" for j in range(64)])
+    res = search_items(index, m, proc, dev, query_text=row, query_image_path="q.png", top_k=3, root_dir=tmp_path)
+    assert res[0].index == 17 and res[0].image_path == "p17" and abs(res[0].score - 1.0) < 1e-3
+    with pytest.raises(FileNotFoundError):
+        search_items(index, m, proc, dev, query_text=row, query_image_path="missing.png", root_dir=tmp_path)

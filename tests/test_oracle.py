@@ -74,3 +74,26 @@ def test_topk_tie_rule_and_tie_comparator():
     assert i.tolist() == [[1, 2, 4]]
     assert S.same_topk_up_to_ties(np.array([1, 4, 2]), np.array([1, 2, 4]), s[0], 1e-9)
     assert not S.same_topk_up_to_ties(np.array([1, 0, 2]), np.array([1, 2, 4]), s[0], 1e-9)
+
+
+def test_fuse_query_oracle_is_seeker_service_rule():
+    """S.fuse_query restates seeker_service.py:148-157; check it against that expression
+    evaluated with torch fp32 exactly as the service writes it (sum over (emb, w) pairs)."""
+    import torch
+    rng = np.random.default_rng(3)
+    t = rng.standard_normal((6, 512)).astype(np.float32)
+    i = rng.standard_normal((6, 512)).astype(np.float32)
+    t /= np.linalg.norm(t, axis=-1, keepdims=True)
+    i /= np.linalg.norm(i, axis=-1, keepdims=True)
+    embs = [(torch.from_numpy(t), 0.5), (torch.from_numpy(i), 0.5)]
+    weighted = sum(w * e for e, w in embs)
+    weighted = weighted / weighted.norm(dim=-1, keepdim=True)
+    np.testing.assert_allclose(S.fuse_query(t, i), weighted.numpy(), atol=2e-7, rtol=0)
+    one = torch.from_numpy(3 * t)
+    np.testing.assert_allclose(S.fuse_query(None, 3 * t), (one / one.norm(dim=-1, keepdim=True)).numpy(),
+                               atol=2e-7, rtol=0)
+    # the fused query of a pair lies between its parts: equal cosine to both at 0.5/0.5
+    f = S.fuse_query(t, i)
+    np.testing.assert_allclose(np.sum(f * t, -1), np.sum(f * i, -1), atol=1e-6)
+    with pytest.raises(ValueError):
+        S.fuse_query(None, None)
