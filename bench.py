@@ -130,29 +130,60 @@ def cpu_baseline(cfg, sd, lora, budget_s: float):
                       f"torch CPU {threads} threads; reference per-item loop (batch 1): {4 / dt1:.2f} pairs/s"}
 
 
-def search_leg(rows: int, queries: int, k: int, device):
+def search_leg(rows: int, queries: int, k: int, device, world: int = 1, rank: int = 0):
+    """BASELINE configs[4]: 10k fp16 queries vs a rows x 512 fp16 index in HBM, top-k.
+    world > 1: the index is row-sharded (rank r holds shard_range(rows, r, world)
+    with global offsets), queries are replicated, each rank searches its shard, one all_gather of
+    the [nq, k] lists and the (score desc, index asc) merge on the GPU give every rank the global
+    top-k. The timed region spans local search + gather + merge, max over ranks."""
+    from clip_lora_match_amd.distributed import shard_range
     from clip_lora_match_amd.search import CosineIndex
     dim = 512
-    idx = CosineIndex(dim, capacity=rows, device=device)
-    g = torch.Generator(device=device).manual_seed(7)
+    start, stop = shard_range(rows, rank, world)
+    idx = CosineIndex(dim, capacity=max(stop - start, 1), device=device)
+    g = torch.Generator(device=device).manual_seed(7 + 1000 * rank)
     chunk = 1 << 20
-    for r0 in range(0, rows, chunk):
-        n = min(chunk, rows - r0)
+    for r0 in range(start, stop, chunk):
+        n = min(chunk, stop - r0)
         x = torch.randn((n, dim), generator=g, device=device)
         idx.append((x / x.norm(dim=-1, keepdim=True)).half())
         del x
+    if world > 1:
+        idx.set_offset(start)
+        g = torch.Generator(device=device).manual_seed(8)   # replicated queries
     q = torch.randn((queries, dim), generator=g, device=device)
     q = (q / q.norm(dim=-1, keepdim=True)).half()
-    idx.search(q[:64], k)
+
+    def run(qq):
+        s, i = idx.search(qq, k)
+        if world > 1:
+            from clip_lora_match_amd.distributed import gather_candidates, merge_topk_gpu
+            s_all, i_all = gather_candidates(s, i)
+            s, i = merge_topk_gpu(s_all, i_all, world, k)
+        return s, i
+
+    run(q[:64])
     torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
     t0 = time.perf_counter()
-    s, i = idx.search(q, k)
+    s, i = run(q)
     torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
     dt = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([dt], dtype=torch.float64, device=device)
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        dt = float(t.item())
     idx.close()
     flops = 2.0 * queries * rows * dim
-    return {"qps": queries / dt, "seconds": dt, "rows": rows, "queries": queries, "k": k, "dim": dim,
-            "index_dtype": "fp16", "tflops": flops / dt / 1e12}
+    out = {"qps": queries / dt, "seconds": dt, "rows": rows, "queries": queries, "k": k, "dim": dim,
+           "index_dtype": "fp16", "tflops": flops / dt / 1e12}
+    if world > 1:
+        out.update({"n_gpus": world, "shard_rows": stop - start,
+                    "parallelism": "row-sharded index, replicated queries, all_gather(top-k) + GPU merge"})
+    return out
 
 
 def l14_leg(device, batch: int = 128, steps: int = 3, warmup: int = 1):
@@ -222,12 +253,15 @@ def main():
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    # modulo: a rehearsal may put several ranks on one GPU; on a full node this is LOCAL_RANK itself
+    local = int(os.environ.get("LOCAL_RANK", "0")) % max(torch.cuda.device_count(), 1)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=dev)
+        # RCCL over xGMI; CLM_DIST_BACKEND=gloo only to rehearse N ranks on one GPU (RCCL refuses that)
+        backend = os.environ.get("CLM_DIST_BACKEND", "nccl")
+        dist.init_process_group(backend, **({"device_id": dev} if backend == "nccl" else {}))
 
     cfg = clm.get_preset("ViT-B/32")   # LoRA r=8, alpha=16 on q,k,v,out (config/lora_config.yaml)
     sd = W.synthetic_state_dict(cfg, 0)
@@ -312,7 +346,7 @@ def main():
         "embeds_per_s": round(2 * pairs_s, 1),
         "step_tflops_per_gpu": round(step_flops / (ms_step * 1e-3) / 1e12, 2),
         "roofline": {
-            "kernel": "gemm_nt_kernel (MFMA 16x16x32, all encoder GEMMs)",
+            "kernel": "gemm_kernel / gemm2_kernel (MFMA 16x16x32, all encoder GEMMs)",
             "bound": "mfma",
             "achieved": round(gemm_flops / (gemm_ms * 1e-3) / 1e12, 2),
             "peak": MFMA_PEAK_TFLOPS,
@@ -327,11 +361,13 @@ def main():
             "kernel_ms_per_step": {k: round(v[0] / nprof, 4) for k, v in prof.items()},
         },
     }
-    if rank == 0 and world == 1 and not args.no_search:
+    if not args.no_search:   # every rank takes part when the index is sharded (world > 1)
         try:
-            result["search"] = search_leg(args.search_rows, args.search_queries, 5, dev)
+            sr = search_leg(args.search_rows, args.search_queries, 5, dev, world, rank)
         except Exception as e:  # report, never hide
-            result["search"] = {"error": repr(e)}
+            sr = {"error": repr(e)}
+        if rank == 0:
+            result["search"] = sr
     if rank == 0 and world == 1 and not args.no_l14:
         try:
             result["l14"] = l14_leg(dev)
