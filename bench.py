@@ -1,36 +1,47 @@
 #!/usr/bin/env python
 """Benchmark: ViT-B/32 + LoRA r=8 encode of 224px images + 77-token captions
-(BASELINE.json configs[1]) on N GPUs, plus an optional cosine top-k search leg
-(configs[4] shape).
+(BASELINE.json configs[1]) on N GPUs, plus the cosine top-k search leg (configs[4]),
+the ViT-L/14@336 leg (configs[3]) and the reference CPU path timed beside them.
 
   python bench.py [--gpus N] [--steps K] [--warmup W]
-  (N > 1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...)
 
-One step = every rank encodes its own batch (default 256 images + 256 captions,
-bf16 operands, LoRA merged) into L2-normalised fp32 embeddings; for N > 1 the
-step ends with the index-build exchange: an RCCL all-gather of every rank's
-embeddings over xGMI (scripts/rebuild_index.py builds the whole index), so per
--GPU work is fixed as N grows ("weak" scaling). Inputs are resident in HBM
-before the timed region. Prints ONE JSON line on rank 0.
+--gpus N > 1 without a torch.distributed launcher around it: bench.py starts its own N ranks
+(python -m torch.distributed.run, 127.0.0.1) before touching the GPU and exits with their
+status. On a box with fewer than N GPUs the ranks rehearse over gloo (RCCL refuses two ranks
+per device) and the line says so ("rehearsal"). Every rank checks that the process group really
+has N ranks.
+
+One step = every rank encodes its own batch (default 256 images + 256 captions, bf16 operands,
+LoRA merged) into L2-normalised fp32 embeddings; for N > 1 the step ends with the index-build
+exchange: an RCCL all-gather of every rank's embeddings over xGMI (scripts/rebuild_index.py
+builds the whole index), so per-GPU work is fixed as N grows ("weak" scaling). Inputs are
+resident in HBM before the timed region. Prints ONE JSON line on rank 0.
 
 value = image+text pairs encoded per second over all ranks.
-roofline = the MFMA GEMM kernel (dominant: ~97% of the step's FLOPs), timed
-live with HIP events on its launch stream in a separate profiled pass.
-cpu_baseline = transformers CLIPModel fp32 on the host cores (the arithmetic
-models/clip_model.py runs) with the restated PEFT LoRA, on a bounded sample.
+roofline = the MFMA GEMM kernels (dominant: ~97% of the step's FLOPs), timed live with HIP
+events on their launch stream in a separate profiled pass; traffic / MFMA busy from the newest
+committed rocprofv3 PMC summary (tools/pmc.sh + tools/pmc_summary.py).
+parity_mode = the same step with fp16 operands (the mode that meets the 1e-3 score bar).
+cpu_baseline = the reference's arithmetic on the host cores: transformers CLIPModel fp32 + the
+restated PEFT LoRA (batched 64 and per item), and search_with_embedding's fp32 q @ E^T + topk
+per single query over the fp16-upcast, re-normalised 10 M-row index (a bounded query subset).
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import re
+import socket
+import subprocess
 import sys
 import time
 
 import numpy as np
 import torch
 
-sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
 
 import clip_lora_match_amd as clm  # noqa: E402
 from clip_lora_match_amd import synthetic as syn  # noqa: E402
@@ -39,10 +50,54 @@ from clip_lora_match_amd.engine import ClipLoraModel  # noqa: E402
 
 MFMA_PEAK_TFLOPS = 2500.0   # dense bf16/fp16 MFMA, MI355X (MI355X_MICROARCH.md chip table)
 HBM_PEAK_GBS = 8000.0
+METRIC = "image+text embeds/sec & cosine top-k QPS, ViT-B/32+LoRA, 1/2/4/8 MI355X"
 
 
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
+
+
+def parse_args(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=256)
+    ap.add_argument("--dtype", default="bfloat16", choices=["bfloat16", "float16"])
+    ap.add_argument("--lora-mode", default="merged", choices=["merged", "unmerged"])
+    ap.add_argument("--cpu-budget", type=float, default=12.0, help="seconds of CPU encode timing")
+    ap.add_argument("--cpu-search-budget", type=float, default=20.0, help="seconds of CPU search timing")
+    ap.add_argument("--cpu-search-queries", type=int, default=100)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--search-rows", type=int, default=10_000_000)
+    ap.add_argument("--search-queries", type=int, default=10_000)
+    ap.add_argument("--no-search", action="store_true")
+    ap.add_argument("--no-l14", action="store_true", help="skip the ViT-L/14@336 (configs[3]) leg")
+    ap.add_argument("--no-parity-mode", action="store_true", help="skip the fp16 parity-mode step")
+    ap.add_argument("--sequential", action="store_true", help="towers back to back on one stream, no graph")
+    ap.add_argument("--split", type=int, default=0, help="sub-batches per tower in encode_pair (0 = library default)")
+    return ap.parse_args(argv)
+
+
+def maybe_spawn(args) -> None:
+    """--gpus N > 1 outside a launcher: run N ranks under torch.distributed.run as a child
+    process and exit with its status. Nothing here touches the GPU (device_count does not
+    initialise it), so the ranks start from a clean process."""
+    if args.gpus <= 1 or "WORLD_SIZE" in os.environ:
+        return
+    ndev = torch.cuda.device_count()
+    env = dict(os.environ)
+    env.setdefault("MASTER_ADDR", "127.0.0.1")
+    if ndev < args.gpus:
+        env["CLM_DIST_BACKEND"] = "gloo"
+        env["CLM_REHEARSAL"] = f"{args.gpus} ranks on {ndev} GPU(s) over gloo: timings are not a scaling measurement"
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    log("bench: launching", " ".join(cmd))
+    sys.exit(subprocess.call(cmd, env=env))
 
 
 def pruned_last_layer() -> bool:
@@ -51,12 +106,13 @@ def pruned_last_layer() -> bool:
     return os.environ.get("CLM_NO_PRUNE", "0") in ("", "0")
 
 
-def flops_per_pair(cfg, pruned=None) -> dict:
-    """Algorithmic FLOPs per image / caption (2 x MAC of every GEMM + full-T^2 attention,
-    LoRA unmerged), SURVEY §8(d). With the last layer pruned, its out_proj / fc1 / fc2 (and
+def flops_per_pair(cfg, pruned=None, lora_merged=False) -> dict:
+    """Algorithmic FLOPs per image / caption (2 x MAC of every GEMM + full-T^2 attention),
+    SURVEY §8(d). LoRA unmerged adds its down/up products; merged LoRA costs nothing (the
+    LoRA column is subtracted). With the last layer pruned, its out_proj / fc1 / fc2 (and
     their LoRA) count one pooled row instead of T."""
     pruned = pruned_last_layer() if pruned is None else pruned
-    r = cfg.lora_r
+    r = 0 if lora_merged else cfg.lora_r
 
     def lora_tok(d, mlp, targets):   # per token and layer: x.A^T (r x fin) + (.)B^T (fout x r)
         dims = {"q_proj": (d, d), "k_proj": (d, d), "v_proj": (d, d), "out_proj": (d, d),
@@ -100,59 +156,134 @@ def gemm_algorithmic_bytes(cfg, B) -> float:
     return tot
 
 
-def cpu_baseline(cfg, sd, lora, budget_s: float):
-    """transformers CLIPModel fp32 on the host cores + restated PEFT LoRA (oracle/hf_ref.py)."""
+def cpu_encode_baseline(cfg, sd, lora, budget_s: float):
+    """transformers CLIPModel fp32 on the host cores + restated PEFT LoRA (oracle/hf_ref.py):
+    the arithmetic of models/clip_model.py encode_image / encode_text. Batched 64 (BASELINE.md
+    §4) for a time budget, and the reference's own per-item calls (batch 1) for 16 + 16 items."""
     from oracle import hf_ref as H
     cores = len(os.sched_getaffinity(0))
     threads = max(1, min(cores, int(os.environ.get("OMP_NUM_THREADS", cores))))
     torch.set_num_threads(threads)
     m = H.hf_model(cfg, sd, lora)
-    n = 16
+    n = 64
     imgs = syn.images_u8(n, cfg.image_size, 777)
     ids = syn.captions(n, cfg.max_pos, cfg.bos_token_id, cfg.eos_token_id, 778)
     pv = H.pixel_values(cfg, imgs)
-    H.encode(m, cfg, pv[:2], ids[:2])  # warm
-    done, t0 = 0, time.perf_counter()
+    H.encode_images(m, pv[:2])
+    H.encode_texts(m, cfg, ids[:2])
+    ti = tt = 0.0
+    batches = 0
     while True:
-        H.encode(m, cfg, pv, ids)
-        done += n
-        if time.perf_counter() - t0 > budget_s:
+        t0 = time.perf_counter()
+        H.encode_images(m, pv)
+        t1 = time.perf_counter()
+        H.encode_texts(m, cfg, ids)
+        t2 = time.perf_counter()
+        ti, tt, batches = ti + t1 - t0, tt + t2 - t1, batches + 1
+        if ti + tt > budget_s:
+            break
+    per = 16
+    t0 = time.perf_counter()
+    for i in range(per):
+        H.encode_images(m, pv[i:i + 1])
+    t1 = time.perf_counter()
+    for i in range(per):
+        H.encode_texts(m, cfg, ids[i:i + 1])
+    t2 = time.perf_counter()
+    pi, pt = per / (t1 - t0), per / (t2 - t1)
+    bi, bt = batches * n / ti, batches * n / tt
+    return {"batched64": {"images_per_s": round(bi, 2), "texts_per_s": round(bt, 2),
+                          "pairs_per_s": round(batches * n / (ti + tt), 2), "batches": batches,
+                          "seconds": round(ti + tt, 2)},
+            "per_item": {"images_per_s": round(pi, 2), "texts_per_s": round(pt, 2),
+                         "pairs_per_s": round(per / (t2 - t0), 2), "calls": 2 * per},
+            "threads": threads, "impl": f"transformers {__import__('transformers').__version__} CLIPModel fp32 "
+                                        "+ PEFT-equivalent LoRA hooks (oracle/hf_ref.py)"}
+
+
+def cpu_search_baseline(host16: torch.Tensor, queries16: torch.Tensor, k: int, max_queries: int, budget_s: float,
+                        gpu_idx: torch.Tensor):
+    """TextSearchIndex semantics on the host cores (search.py:36,68,93-99): the fp16 index upcast
+    to fp32 and re-normalised once, then per single query q / ||q||, sims = q @ E^T, topk(k).
+    Also checks the GPU's top-k for the same queries (indices equal up to fp32 near-ties)."""
+    t_prep = time.perf_counter()
+    E = host16.float()
+    E /= E.norm(dim=-1, keepdim=True)
+    t_prep = time.perf_counter() - t_prep
+    done, t0 = 0, time.perf_counter()
+    match = 0
+    for qi in range(min(max_queries, queries16.shape[0])):
+        q = queries16[qi:qi + 1].float()
+        q = q / q.norm(dim=-1, keepdim=True)
+        sims = q @ E.T
+        vals, idx = torch.topk(sims, k, dim=-1)
+        done += 1
+        # parity of this query: GPU indices vs the reference's, allowing fp32 near-ties (2e-6)
+        g = gpu_idx[qi]
+        if torch.equal(idx[0], g):
+            match += 1
+        else:
+            cand = torch.unique(torch.cat([idx[0], g]))
+            ex = (E[cand].double() @ q[0].double())
+            exd = dict(zip(cand.tolist(), ex.tolist()))
+            sa = torch.tensor([exd[int(i)] for i in idx[0]])
+            sb = torch.tensor([exd[int(i)] for i in g])
+            if float((sa - sb).abs().max()) <= 2e-6:
+                match += 1
+        if time.perf_counter() - t0 > budget_s and done >= 10:
             break
     dt = time.perf_counter() - t0
-    # the reference's own call pattern: one image / one caption per call (clip_model.py:89-150)
-    t1 = time.perf_counter()
-    for i in range(4):
-        H.encode(m, cfg, pv[i:i + 1], ids[i:i + 1])
-    dt1 = time.perf_counter() - t1
-    return {"value": done / dt, "unit": "pairs/s", "cores": threads, "kind": "reference",
-            "sample": f"{done} image+caption pairs in batches of {n} ({dt:.1f} s), transformers "
-                      f"{__import__('transformers').__version__} CLIPModel fp32 + PEFT-equivalent LoRA hooks, "
-                      f"torch CPU {threads} threads; reference per-item loop (batch 1): {4 / dt1:.2f} pairs/s"}
+    del E
+    return {"qps": round(done / dt, 3), "ms_per_query": round(dt / done * 1e3, 2), "queries": done,
+            "rows": host16.shape[0], "k": k, "prep_s": round(t_prep, 2),
+            "gpu_topk_matches_reference": f"{match}/{done}",
+            "impl": "torch CPU fp32: index.float() / ||row|| once; per query q/||q||, q @ E^T, topk"}
 
 
-def search_leg(rows: int, queries: int, k: int, device, world: int = 1, rank: int = 0):
-    """BASELINE configs[4]: 10k fp16 queries vs a rows x 512 fp16 index in HBM, top-k.
+def search_leg(rows: int, queries: int, k: int, device, world: int = 1, rank: int = 0, keep_host: bool = False):
+    """BASELINE configs[4]: 10k fp16 query embeddings vs a rows x 512 fp16 index in HBM, top-k
+    by exact cosine (fp16 MFMA pass + exact re-score of the candidates).
     world > 1: the index is row-sharded (rank r holds shard_range(rows, r, world)
     with global offsets), queries are replicated, each rank searches its shard, one all_gather of
     the [nq, k] lists and the (score desc, index asc) merge on the GPU give every rank the global
-    top-k. The timed region spans local search + gather + merge, max over ranks."""
+    top-k. The timed region spans local search + gather + merge, max over ranks.
+    Every rank reports whether its shard built; all skip together if one failed (no rank is left
+    waiting in a collective)."""
     from clip_lora_match_amd.distributed import shard_range
     from clip_lora_match_amd.search import CosineIndex
     dim = 512
     start, stop = shard_range(rows, rank, world)
-    idx = CosineIndex(dim, capacity=max(stop - start, 1), device=device)
-    g = torch.Generator(device=device).manual_seed(7 + 1000 * rank)
-    chunk = 1 << 20
-    for r0 in range(start, stop, chunk):
-        n = min(chunk, stop - r0)
-        x = torch.randn((n, dim), generator=g, device=device)
-        idx.append((x / x.norm(dim=-1, keepdim=True)).half())
-        del x
+    err = None
+    idx = None
+    host16 = None
+    try:
+        idx = CosineIndex(dim, capacity=max(stop - start, 1), device=device)
+        g = torch.Generator(device=device).manual_seed(7 + 1000 * rank)
+        if keep_host:
+            host16 = torch.empty((stop - start, dim), dtype=torch.float16)
+        chunk = 1 << 20
+        for r0 in range(start, stop, chunk):
+            n = min(chunk, stop - r0)
+            x = torch.randn((n, dim), generator=g, device=device)
+            xh = (x / x.norm(dim=-1, keepdim=True)).half()
+            idx.append(xh)
+            if host16 is not None:
+                host16[r0 - start: r0 - start + n] = xh.cpu()
+            del x, xh
+        if world > 1:
+            idx.set_offset(start)
+            g = torch.Generator(device=device).manual_seed(8)   # replicated queries
+        q = torch.randn((queries, dim), generator=g, device=device)
+        q = (q / q.norm(dim=-1, keepdim=True)).half()
+    except Exception as e:   # reported, never hidden
+        err = repr(e)
     if world > 1:
-        idx.set_offset(start)
-        g = torch.Generator(device=device).manual_seed(8)   # replicated queries
-    q = torch.randn((queries, dim), generator=g, device=device)
-    q = (q / q.norm(dim=-1, keepdim=True)).half()
+        ok = torch.tensor([0 if err else 1], dtype=torch.int32, device=device)
+        torch.distributed.all_reduce(ok, op=torch.distributed.ReduceOp.MIN)
+        if int(ok.item()) == 0:
+            return {"error": err or "another rank failed to build its shard"}, None, None, None
+    elif err:
+        return {"error": err}, None, None, None
 
     def run(qq):
         s, i = idx.search(qq, k)
@@ -176,14 +307,17 @@ def search_leg(rows: int, queries: int, k: int, device, world: int = 1, rank: in
         t = torch.tensor([dt], dtype=torch.float64, device=device)
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
         dt = float(t.item())
+    st = idx.stats()
     idx.close()
     flops = 2.0 * queries * rows * dim
-    out = {"qps": queries / dt, "seconds": dt, "rows": rows, "queries": queries, "k": k, "dim": dim,
-           "index_dtype": "fp16", "tflops": flops / dt / 1e12}
+    out = {"qps": round(queries / dt, 1), "seconds": round(dt, 4), "rows": rows, "queries": queries, "k": k,
+           "dim": dim, "index_dtype": "fp16", "tflops": round(flops / dt / 1e12, 1),
+           "scores": "exact cosine (fp16 MFMA candidate pass + fp64 re-score), order (score desc, index asc)",
+           "paths": st}
     if world > 1:
         out.update({"n_gpus": world, "shard_rows": stop - start,
                     "parallelism": "row-sharded index, replicated queries, all_gather(top-k) + GPU merge"})
-    return out
+    return out, host16, q.cpu(), i.cpu()
 
 
 def l14_leg(device, batch: int = 128, steps: int = 3, warmup: int = 1):
@@ -213,55 +347,79 @@ def l14_leg(device, batch: int = 128, steps: int = 3, warmup: int = 1):
     prof = m.prof_read()
     m.prof_enable(False)
     m.close()
-    fp = flops_per_pair(cfg)["image"]
+    fp = flops_per_pair(cfg, lora_merged=True)["image"]
     g_ms, g_flops, _ = prof["gemm"]
+    a_ms, a_flops, _ = prof["attn"]
     return {"config": "ViT-L/14@336 + LoRA r=16 (q,k,v,out,fc1,fc2) merged, bf16, batch 128, image tower",
             "images_per_s": round(batch / dt, 1), "ms_per_step": round(dt * 1e3, 3),
             "step_tflops": round(batch * fp / dt / 1e12, 1),
             "gemm_tflops": round(g_flops / (g_ms * 1e-3) / 1e12, 1),
+            "attn_tflops": round(a_flops / (a_ms * 1e-3) / 1e12, 1),
             "kernel_ms": {k: round(v[0], 3) for k, v in prof.items()}}
 
 
-def pmc_traffic():
-    """HBM bytes per GEMM launch from the newest committed PMC summary (tools/pmc_summary.py),
-    or None when no counter run has been recorded."""
+def newest_profile(pattern: str):
+    """The newest committed summary matching profiles/r<round>_v<version>_<pattern>, ordered by
+    (round, version) numerically (a lexicographic sort would put v9 after v11)."""
     import glob
-    files = sorted(glob.glob(os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "*_pmc_summary.json")))
-    if not files:
-        return None, None
-    d = json.load(open(files[-1]))
-    return d.get("gemm_mean_hbm_bytes_per_launch"), os.path.basename(files[-1])
+    best, key = None, None
+    for f in glob.glob(os.path.join(REPO, "profiles", f"*_{pattern}")):
+        m = re.match(r"r(\d+)_v(\d+)", os.path.basename(f))
+        if not m:
+            continue
+        kk = (int(m.group(1)), int(m.group(2)))
+        if key is None or kk > key:
+            best, key = f, kk
+    return best
+
+
+def pmc_summary():
+    f = newest_profile("pmc_summary.json")
+    if not f:
+        return {}, None
+    return json.load(open(f)), os.path.basename(f)
+
+
+def parity_mode_leg(cfg, sd, lora, dev, B, imgs, ids, steps, warmup, lora_mode):
+    """The same encode step with fp16 operands: the precision that meets the 1e-3 score bar."""
+    m = ClipLoraModel(cfg, device=dev, compute_dtype="float16", lora_mode=lora_mode, max_batch=B)
+    m.load_tensors(sd)
+    m.load_tensors(lora)
+    m.finalize()
+    oi = torch.empty((B, cfg.proj_dim), dtype=torch.float32, device=dev)
+    ot = torch.empty_like(oi)
+    for _ in range(warmup):
+        m.encode_pair(imgs, ids, out_img=oi, out_txt=ot, graph=True)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        m.encode_pair(imgs, ids, out_img=oi, out_txt=ot, graph=True)
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / steps
+    m.close()
+    return {"dtype": "fp16", "value": round(B / dt, 1), "unit": "image+text pairs/s", "ms_per_step": round(dt * 1e3, 4),
+            "note": "fp16 operands, fp32 accumulate/residual/LN/softmax: scores within 1e-3 of the fp32 reference"}
 
 
 def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--batch", type=int, default=256)
-    ap.add_argument("--dtype", default="bfloat16", choices=["bfloat16", "float16"])
-    ap.add_argument("--lora-mode", default="merged", choices=["merged", "unmerged"])
-    ap.add_argument("--cpu-budget", type=float, default=12.0)
-    ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--search-rows", type=int, default=10_000_000)
-    ap.add_argument("--search-queries", type=int, default=10_000)
-    ap.add_argument("--no-search", action="store_true")
-    ap.add_argument("--no-l14", action="store_true", help="skip the ViT-L/14@336 (configs[3]) leg")
-    ap.add_argument("--sequential", action="store_true", help="towers back to back on one stream, no graph")
-    ap.add_argument("--split", type=int, default=0, help="sub-batches per tower in encode_pair (0 = library default)")
-    args = ap.parse_args()
-
+    args = parse_args()
+    maybe_spawn(args)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py --gpus {args.gpus} but the launcher started {world} rank(s)")
     # modulo: a rehearsal may put several ranks on one GPU; on a full node this is LOCAL_RANK itself
     local = int(os.environ.get("LOCAL_RANK", "0")) % max(torch.cuda.device_count(), 1)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
+    backend = None
     if world > 1:
         import torch.distributed as dist
-        # RCCL over xGMI; CLM_DIST_BACKEND=gloo only to rehearse N ranks on one GPU (RCCL refuses that)
+        # RCCL over xGMI; CLM_DIST_BACKEND=gloo only to rehearse N ranks on fewer GPUs
         backend = os.environ.get("CLM_DIST_BACKEND", "nccl")
         dist.init_process_group(backend, **({"device_id": dev} if backend == "nccl" else {}))
+        if dist.get_world_size() != args.gpus:
+            raise SystemExit(f"process group has {dist.get_world_size()} ranks, --gpus {args.gpus}")
 
     cfg = clm.get_preset("ViT-B/32")   # LoRA r=8, alpha=16 on q,k,v,out (config/lora_config.yaml)
     sd = W.synthetic_state_dict(cfg, 0)
@@ -283,8 +441,7 @@ def main():
             model.encode_pixels(imgs, out=emb[:B])
             model.encode_ids(ids, out=emb[B:])
         else:   # towers concurrently on two streams, replayed from a captured hipGraph
-            model.encode_pair(imgs, ids, out_img=emb[:B], out_txt=emb[B:], graph=not profiling[0],
-                               split=args.split)
+            model.encode_pair(imgs, ids, out_img=emb[:B], out_txt=emb[B:], graph=True, split=args.split)
         if world > 1:
             torch.distributed.all_gather_into_tensor(gathered, emb)
 
@@ -318,13 +475,13 @@ def main():
     prof = model.prof_read()
     model.prof_enable(False)
     gemm_ms, gemm_flops, gemm_n = prof["gemm"]
-    fp = flops_per_pair(cfg)
-    traffic, traffic_src = pmc_traffic()
+    fp = flops_per_pair(cfg, lora_merged=args.lora_mode == "merged")
+    pmc, pmc_src = pmc_summary()
     gemm_bytes = gemm_algorithmic_bytes(cfg, B) * nprof
     step_flops = B * (fp["image"] + fp["caption"])
 
     result = {
-        "metric": "image+text embeds/sec & cosine top-k QPS, ViT-B/32+LoRA, 1/2/4/8 MI355X",
+        "metric": METRIC,
         "value": round(pairs_s, 1),
         "unit": "image+text pairs/s",
         "n_gpus": world,
@@ -352,20 +509,33 @@ def main():
             "peak": MFMA_PEAK_TFLOPS,
             "unit": "TFLOP/s",
             "frac": round(gemm_flops / (gemm_ms * 1e-3) / 1e12 / MFMA_PEAK_TFLOPS, 4),
-            "traffic": traffic,
+            "traffic": pmc.get("gemm_mean_hbm_bytes_per_launch"),
             "traffic_unit": "bytes per launch (PMC: 2*FETCH_SIZE + WRITE_SIZE, gfx950-corrected)",
-            "traffic_source": traffic_src,
+            "traffic_source": pmc_src,
+            "mfma_busy_frac": pmc.get("gemm_mfma_busy_frac"),
+            "mfma_busy_source": pmc_src if pmc.get("gemm_mfma_busy_frac") is not None else None,
             "algorithmic_bytes_per_launch": round(gemm_bytes / max(gemm_n, 1)),
             "avg_launch_us": round(gemm_ms / gemm_n * 1e3, 2),
             "launches_per_step": gemm_n // nprof,
             "kernel_ms_per_step": {k: round(v[0] / nprof, 4) for k, v in prof.items()},
         },
     }
-    if not args.no_search:   # every rank takes part when the index is sharded (world > 1)
+    if world > 1:
+        result["dist"] = {"backend": backend, "world_size": torch.distributed.get_world_size()}
+        if os.environ.get("CLM_REHEARSAL"):
+            result["rehearsal"] = os.environ["CLM_REHEARSAL"]
+    if rank == 0 and world == 1 and not args.no_parity_mode:
         try:
-            sr = search_leg(args.search_rows, args.search_queries, 5, dev, world, rank)
+            result["parity_mode"] = parity_mode_leg(cfg, sd, lora, dev, B, imgs, ids, args.steps, args.warmup,
+                                                    args.lora_mode)
         except Exception as e:  # report, never hide
-            sr = {"error": repr(e)}
+            result["parity_mode"] = {"error": repr(e)}
+    model.close()
+    host16 = qs_host = gpu_i = None
+    if not args.no_search:   # every rank takes part when the index is sharded (world > 1)
+        keep = rank == 0 and world == 1 and not args.no_cpu_baseline
+        sr, host16, qs_host, gpu_i = search_leg(args.search_rows, args.search_queries, 5, dev, world, rank,
+                                                keep_host=keep)
         if rank == 0:
             result["search"] = sr
     if rank == 0 and world == 1 and not args.no_l14:
@@ -374,10 +544,21 @@ def main():
         except Exception as e:  # report, never hide
             result["l14"] = {"error": repr(e)}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        result["cpu_baseline"] = cpu_baseline(cfg, sd, lora, args.cpu_budget)
+        enc = cpu_encode_baseline(cfg, sd, lora, args.cpu_budget)
+        cb = {"value": enc["batched64"]["pairs_per_s"], "unit": "image+text pairs/s",
+              "cores": enc["threads"], "kind": "reference",
+              "sample": f"{enc['batched64']['batches']} batches of 64 images + 64 captions "
+                        f"({enc['batched64']['seconds']} s) of configs[1] (B/32 + LoRA r=8), {enc['impl']}, "
+                        f"{enc['threads']} threads; per-item (the reference's encode_image/encode_text pattern): "
+                        f"{enc['per_item']['pairs_per_s']} pairs/s over {enc['per_item']['calls']} calls",
+              "encode": enc}
+        if host16 is not None:
+            cb["search"] = cpu_search_baseline(host16, qs_host, 5, args.cpu_search_queries, args.cpu_search_budget,
+                                               gpu_i)
+            cb["search"]["threads"] = enc["threads"]
+        result["cpu_baseline"] = cb
     if rank == 0:
         print(json.dumps(result), flush=True)
-    model.close()
     if world > 1:
         torch.distributed.destroy_process_group()
 

@@ -65,6 +65,7 @@ def lib():
         "clm_load_tensor": (c_int, [c_void_p, c_char_p, c_void_p, c_int, POINTER(c_int64), c_int]),
         "clm_finalize": (c_int, [c_void_p]),
         "clm_set_lora_enabled": (c_int, [c_void_p, c_int]),
+        "clm_set_lora": (c_int, [c_void_p, c_int, ctypes.c_float, c_uint32]),
         "clm_encode_image": (c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p, c_int, c_int, c_void_p]),
         "clm_encode_text": (c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p, c_int, c_int, c_void_p]),
         "clm_encode_pair": (c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p, c_int, c_int, c_void_p, c_void_p,
@@ -78,6 +79,7 @@ def lib():
         "clm_index_read": (c_int, [c_void_p, c_int64, c_int64, c_void_p, c_void_p]),
         "clm_index_search": (c_int, [c_void_p, c_void_p, c_int, c_int64, c_int, c_void_p, c_void_p, c_void_p]),
         "clm_index_stats": (c_int, [c_void_p, POINTER(c_int64), POINTER(c_int64), POINTER(c_int64)]),
+        "clm_index_stats2": (c_int, [c_void_p, POINTER(c_int64), c_int]),
         "clm_cosine_scores": (c_int, [c_int, c_void_p, c_int64, c_void_p, c_int64, c_int, c_void_p, c_void_p]),
         "clm_topk_merge": (c_int, [c_int, c_void_p, c_void_p, c_int64, c_int, c_int, c_int, c_void_p, c_void_p,
                                    c_void_p]),
@@ -105,9 +107,10 @@ def lib():
 
 
 EXPORTED = (
-    "clm_ctx_create", "clm_ctx_destroy", "clm_load_tensor", "clm_finalize", "clm_set_lora_enabled",
+    "clm_ctx_create", "clm_ctx_destroy", "clm_load_tensor", "clm_finalize", "clm_set_lora_enabled", "clm_set_lora",
     "clm_encode_image", "clm_encode_text", "clm_encode_pair", "clm_index_create", "clm_index_destroy", "clm_index_append",
     "clm_index_size", "clm_index_reset", "clm_index_set_offset", "clm_index_read", "clm_index_search", "clm_index_stats",
+    "clm_index_stats2",
     "clm_cosine_scores", "clm_topk_merge", "clm_l2_normalize", "clm_fuse_queries", "clm_last_error", "clm_version",
     "clm_model_desc_size", "clm_prof_enable", "clm_prof_read", "clm_gemm", "clm_gemm_num_configs",
     "clm_attention", "clm_debug_set",

@@ -9,14 +9,17 @@ return types and error behaviour), running on the gfx950 HIP kernels.
   encode_text         models/clip_model.py:121-150 -> (D,) float32 CPU, unit norm
 
 Differences forced by the environment (no network, no peft, no CPU path):
-  * CLIPModel.from_pretrained(name) becomes: a local transformers checkpoint
-    directory if one is configured (`model.weights_dir` in the YAML, the
-    `weights_dir` argument or $CLM_WEIGHTS_DIR), else the deterministic
-    synthetic weights of weights.synthetic_state_dict (announced on stdout, as
-    the reference announces its own loading steps).
-  * PeftModel.from_pretrained(dir) reads the PEFT on-disk adapter format
-    directly (weights.load_peft_adapter); lora_weights_path="synthetic" attaches
-    the deterministic non-zero synthetic adapter.
+  * CLIPModel.from_pretrained(name) fetches from the Hub, which is unreachable here, so the
+    base weights come from a local transformers checkpoint directory: `model.weights_dir`
+    in the YAML, the `weights_dir` argument or $CLM_WEIGHTS_DIR. The value "synthetic"
+    selects the deterministic synthetic weights of weights.synthetic_state_dict (tests,
+    benchmarks); with none of these set the load fails with OSError, as from_pretrained
+    does offline -- never a silent substitute.
+  * PeftModel.from_pretrained(dir) reads the PEFT on-disk adapter format directly
+    (weights.load_peft_adapter); lora_weights_path="synthetic" attaches the deterministic
+    non-zero synthetic adapter. A missing / unset LoRA path prints the reference's warning
+    and continues without LoRA (models/clip_model.py:70-75); strict_lora=True (or
+    $CLM_STRICT_LORA=1) raises instead, as the src/models/clip_model.py:54-59 variant does.
   * device "cpu" in the YAML (the shipped config) still runs on the GPU: this
     package has no CPU compute path.
 """
@@ -67,6 +70,21 @@ def _get_dtype(dtype_str: str, device: torch.device) -> str:
     return "float16"
 
 
+def _base_weights(model_name: str, cfg, weights_dir, model_cfg: dict, seed: int):
+    src = weights_dir or model_cfg.get("weights_dir") or os.environ.get("CLM_WEIGHTS_DIR")
+    if src is None:
+        raise OSError(
+            f"no local checkpoint for '{model_name}': CLIPModel.from_pretrained needs the Hub, which is "
+            "unreachable here. Point model.weights_dir (YAML), weights_dir= or $CLM_WEIGHTS_DIR at a "
+            "transformers checkpoint directory, or set it to 'synthetic' for the deterministic synthetic weights")
+    if str(src) == "synthetic":
+        print(f"[clip_model] using deterministic synthetic weights for '{model_name}' (seed={seed})")
+        return W.synthetic_state_dict(cfg, seed)
+    if not Path(src).exists():
+        raise FileNotFoundError(f"CLIP checkpoint directory not found: {src}")
+    return W.load_hf_checkpoint(src)
+
+
 def load_clip_model(
     config_path: Union[str, Path] = "config/clip_config.yaml",
     use_lora: bool = False,
@@ -77,6 +95,7 @@ def load_clip_model(
     lora_mode: str = "merged",
     compute_dtype: Optional[str] = None,
     seed: int = 0,
+    strict_lora: Optional[bool] = None,
 ) -> Tuple[ClipLoraModel, ClipProcessor, torch.device]:
     """Load CLIP (+ optional LoRA) onto the GPU; returns (model, processor, device)."""
     config = _load_clip_config(config_path)
@@ -85,15 +104,11 @@ def load_clip_model(
     device = _get_device(model_cfg.get("device"))
     dtype = compute_dtype or _get_dtype(model_cfg.get("dtype", "float16"), device)
     cfg = get_preset(model_name)
+    if strict_lora is None:
+        strict_lora = os.environ.get("CLM_STRICT_LORA", "0") not in ("", "0")
 
     print(f"[clip_model] Loading CLIP model '{model_name}' on device: {device} (dtype={dtype})")
-    wdir = weights_dir or model_cfg.get("weights_dir") or os.environ.get("CLM_WEIGHTS_DIR")
-    if wdir and Path(wdir).exists():
-        sd = W.load_hf_checkpoint(wdir)
-    else:
-        print(f"[clip_model] no local checkpoint for '{model_name}' (offline); using deterministic "
-              f"synthetic weights (seed={seed})")
-        sd = W.synthetic_state_dict(cfg, seed)
+    sd = _base_weights(model_name, cfg, weights_dir, model_cfg, seed)
 
     lora = None
     if use_lora:
@@ -101,6 +116,8 @@ def load_clip_model(
         if lora_weights_path is None:
             lora_weights_path = paths_cfg.get("lora_weights_dir")
         if lora_weights_path is None:
+            if strict_lora:
+                raise ValueError("use_lora=True but lora_weights_path is not set")
             print("[clip_model] use_lora=True tetapi lora_weights_path tidak diset, lanjut tanpa LoRA.")
         elif str(lora_weights_path) == "synthetic":
             lora = W.synthetic_lora(cfg, seed + 1)
@@ -108,6 +125,8 @@ def load_clip_model(
         else:
             lora_path = Path(lora_weights_path)
             if not lora_path.exists():
+                if strict_lora:
+                    raise FileNotFoundError(f"LoRA weights not found: {lora_path}")
                 print(f"[clip_model] LoRA weights tidak ditemukan di: {lora_path}, lanjut tanpa LoRA.")
             else:
                 print(f"[clip_model] Loading LoRA weights from: {lora_path}")

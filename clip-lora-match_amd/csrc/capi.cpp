@@ -197,14 +197,23 @@ struct clm_ctx {
 struct clm_index {
   int dev = 0;
   int64_t cap = 0, n = 0, dim = 0, offset = 0;
+  // MFMA-pass operands: fp16 rows (f16 appends: the rows as given; f32 appends: the rows
+  // normalised in fp32, then rounded) + fp32 inverse norms of those fp16 rows
   u16* rows = nullptr;
   float* inv = nullptr;
-  // search workspaces (grown on demand): ws = query staging, ws2 = path buffers
+  // the caller's fp32 rows, kept once any f32 rows were appended (f16 appends upcast into it):
+  // the exact re-scoring reads these; without them the fp16 rows ARE the caller's rows
+  float* rows32 = nullptr;
+  // search workspaces (grown on demand): ws = query staging, ws2 = per-query-block buffers,
+  // ws3 = chunked score matrices of the exact scans
   void* ws = nullptr; size_t ws_bytes = 0;
   void* ws2 = nullptr; size_t ws2_bytes = 0;
+  void* ws3 = nullptr; size_t ws3_bytes = 0;
   // strided row sample for the threshold pass, rebuilt when n changes
   u16* samp = nullptr; float* samp_inv = nullptr; int64_t samp_S = 0, samp_n = -1, samp_cap = 0;
-  int64_t search_stats[3] = {0, 0, 0};   // filtered queries, exact queries, overflow fallbacks
+  // queries served by: [0] sampled bounded search, [1] the full exact scan, [2] overflow re-runs,
+  // [3] bounded search with the chunked fp16 scan as step 1
+  int64_t search_stats[4] = {0, 0, 0, 0};
 };
 
 namespace {
@@ -773,6 +782,18 @@ int clm_finalize(clm_ctx* ctx) {
   return CLM_OK;
 }
 
+int clm_set_lora(clm_ctx* ctx, int r, float alpha, uint32_t targets) {
+  if (!ctx) return fail(CLM_E_ARG, "null ctx");
+  if (r < 0 || r > 64) return fail(CLM_E_ARG, "lora_r must be in [0, 64]");
+  if (targets & ~(uint32_t)(CLM_LORA_Q | CLM_LORA_K | CLM_LORA_V | CLM_LORA_OUT | CLM_LORA_FC1 | CLM_LORA_FC2))
+    return fail(CLM_E_ARG, "unknown LoRA target bits");
+  ctx->desc.lora_r = r;
+  ctx->desc.lora_alpha = alpha;
+  ctx->desc.lora_targets = r > 0 ? targets : 0u;
+  ctx->finalized = false;   // the adapter tensors are loaded next, then clm_finalize
+  return CLM_OK;
+}
+
 int clm_set_lora_enabled(clm_ctx* ctx, int enabled) {
   if (!ctx) return fail(CLM_E_ARG, "null ctx");
   ctx->lora_enabled = enabled != 0;
@@ -967,8 +988,12 @@ int clm_encode_pair(clm_ctx* ctx, const void* pixels, int pix_layout, int n_img,
 }
 
 // ------------------------------------------------------------------ index ---
+// HBM-resident cosine index behind TextSearchIndex / top_k_similar (src/embedding/search.py:
+// 24-115, similarity.py:36-58). Search = an fp16 MFMA pass that bounds the candidates, then an
+// exact fp64 re-score of the candidates against the caller's own rows (see clm_index_search).
 int clm_index_create(int hip_device, int64_t capacity, int dim, clm_index** out) {
-  if (!out || capacity < 0 || dim <= 0 || dim % 64) return fail(CLM_E_ARG, "bad capacity/dim (dim must be a multiple of 64)");
+  if (!out || capacity < 0 || dim <= 0 || dim % 64 || dim > 1024)
+    return fail(CLM_E_ARG, "bad capacity/dim (dim must be a multiple of 64, <= 1024)");
   DeviceGuard g(hip_device);
   clm_index* x = new clm_index();
   x->dev = hip_device;
@@ -989,12 +1014,9 @@ int clm_index_destroy(clm_index* x) {
   if (!x) return CLM_OK;
   DeviceGuard g(x->dev);
   (void)hipDeviceSynchronize();
-  if (x->rows) (void)hipFree(x->rows);
-  if (x->inv) (void)hipFree(x->inv);
-  if (x->ws) (void)hipFree(x->ws);
-  if (x->ws2) (void)hipFree(x->ws2);
-  if (x->samp) (void)hipFree(x->samp);
-  if (x->samp_inv) (void)hipFree(x->samp_inv);
+  for (void* p : {(void*)x->rows, (void*)x->inv, (void*)x->rows32, x->ws, x->ws2, x->ws3, (void*)x->samp,
+                  (void*)x->samp_inv})
+    if (p) (void)hipFree(p);
   delete x;
   return CLM_OK;
 }
@@ -1004,14 +1026,22 @@ static int index_grow(clm_index* x, int64_t need_rows) {
   int64_t nc = std::max<int64_t>(need_rows, x->cap * 2);
   u16* nr = nullptr;
   float* ni = nullptr;
+  float* n32 = nullptr;
   if (hipMalloc(&nr, (size_t)nc * x->dim * sizeof(u16)) != hipSuccess ||
-      hipMalloc(&ni, (size_t)nc * sizeof(float)) != hipSuccess) {
+      hipMalloc(&ni, (size_t)nc * sizeof(float)) != hipSuccess ||
+      (x->rows32 && hipMalloc(&n32, (size_t)nc * x->dim * sizeof(float)) != hipSuccess)) {
     (void)hipGetLastError();
     if (nr) (void)hipFree(nr);
+    if (ni) (void)hipFree(ni);
     return fail(CLM_E_OOM, "index grow failed");
   }
   HIPCHK(hipMemcpy(nr, x->rows, (size_t)x->n * x->dim * sizeof(u16), hipMemcpyDeviceToDevice));
   HIPCHK(hipMemcpy(ni, x->inv, (size_t)x->n * sizeof(float), hipMemcpyDeviceToDevice));
+  if (n32) {
+    HIPCHK(hipMemcpy(n32, x->rows32, (size_t)x->n * x->dim * sizeof(float), hipMemcpyDeviceToDevice));
+    (void)hipFree(x->rows32);
+    x->rows32 = n32;
+  }
   (void)hipFree(x->rows);
   (void)hipFree(x->inv);
   x->rows = nr;
@@ -1029,6 +1059,16 @@ int clm_index_append(clm_index* x, const void* rows, int dtype, int64_t n, void*
   HIPCHK(hipStreamSynchronize(st));
   int r = index_grow(x, x->n + n);
   if (r) return r;
+  x->samp_n = -1;   // the threshold sample is rebuilt from the new row set
+  if (dtype == CLM_F32 && !x->rows32) {
+    // first fp32 rows: keep an fp32 copy from now on; the rows so far were fp16 as given
+    if (hipMalloc(&x->rows32, (size_t)x->cap * x->dim * sizeof(float)) != hipSuccess) {
+      (void)hipGetLastError();
+      x->rows32 = nullptr;
+      return fail(CLM_E_OOM, "fp32 row copy allocation failed");
+    }
+    KCHK(f16_to_f32_rows(x->rows, x->n, (int)x->dim, x->rows32, st));
+  }
   const size_t bytes = (size_t)n * x->dim * dtype_size(dtype);
   const void* src = rows;
   void* tmp = nullptr;
@@ -1037,15 +1077,22 @@ int clm_index_append(clm_index* x, const void* rows, int dtype, int64_t n, void*
     HIPCHK(hipMemcpyAsync(tmp, rows, bytes, hipMemcpyHostToDevice, st));
     src = tmp;
   }
-  // inverse norm of the fp16-ROUNDED row: the reference re-normalises the fp32
-  // upcast of the stored rows at load (search.py:36,68)
-  hipError_t e = rows_to_f16(src, dtype == CLM_F32 ? 0 : 1, n, (int)x->dim, x->rows + (size_t)x->n * x->dim,
-                             x->inv + x->n, st, 0);
+  hipError_t e = hipSuccess;
+  if (x->rows32) {
+    float* dst = x->rows32 + (size_t)x->n * x->dim;
+    e = dtype == CLM_F32 ? hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, st)
+                         : f16_to_f32_rows((const u16*)src, n, (int)x->dim, dst, st);
+  }
+  // fp16 MFMA operands: f32 rows are normalised first (no fp16 overflow / subnormal loss);
+  // f16 rows are kept as given (exact) with the inverse norms of those rows
+  if (e == hipSuccess)
+    e = rows_to_f16(src, dtype == CLM_F32 ? 0 : 1, n, (int)x->dim, x->rows + (size_t)x->n * x->dim, x->inv + x->n,
+                    st, dtype == CLM_F32 ? 2 : 0);
   if (tmp) {
     (void)hipStreamSynchronize(st);
     (void)hipFree(tmp);
   }
-  if (e != hipSuccess) return fail(CLM_E_HIP, std::string("rows_to_f16: ") + hipGetErrorString(e));
+  if (e != hipSuccess) return fail(CLM_E_HIP, std::string("index append: ") + hipGetErrorString(e));
   x->n += n;
   return CLM_OK;
 }
@@ -1055,6 +1102,7 @@ int64_t clm_index_size(const clm_index* x) { return x ? x->n : -1; }
 int clm_index_reset(clm_index* x) {
   if (!x) return fail(CLM_E_ARG, "null index");
   x->n = 0;
+  x->samp_n = -1;   // never reuse a sample of the previous rows
   return CLM_OK;
 }
 
@@ -1069,15 +1117,21 @@ int clm_index_read(clm_index* x, int64_t start, int64_t n, float* dst, void* str
   if (n == 0) return CLM_OK;
   DeviceGuard g(x->dev);
   hipStream_t st = (hipStream_t)stream;
-  std::vector<u16> h((size_t)n * x->dim);
-  HIPCHK(hipMemcpyAsync(h.data(), x->rows + (size_t)start * x->dim, h.size() * 2, hipMemcpyDeviceToHost, st));
-  HIPCHK(hipStreamSynchronize(st));
-  std::vector<float> f(h.size());
-  for (size_t i = 0; i < h.size(); ++i) f[i] = host_f16_to_f32(h[i]);
-  if (is_device_ptr(dst)) {
-    HIPCHK(hipMemcpy(dst, f.data(), f.size() * 4, hipMemcpyHostToDevice));
+  const size_t cnt = (size_t)n * x->dim;
+  std::vector<float> f(cnt);
+  if (x->rows32) {
+    HIPCHK(hipMemcpyAsync(f.data(), x->rows32 + (size_t)start * x->dim, cnt * 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
   } else {
-    std::memcpy(dst, f.data(), f.size() * 4);
+    std::vector<u16> h(cnt);
+    HIPCHK(hipMemcpyAsync(h.data(), x->rows + (size_t)start * x->dim, cnt * 2, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    for (size_t i = 0; i < cnt; ++i) f[i] = host_f16_to_f32(h[i]);
+  }
+  if (is_device_ptr(dst)) {
+    HIPCHK(hipMemcpy(dst, f.data(), cnt * 4, hipMemcpyHostToDevice));
+  } else {
+    std::memcpy(dst, f.data(), cnt * 4);
   }
   return CLM_OK;
 }
@@ -1095,10 +1149,17 @@ static int grow(void** p, size_t* cap, size_t bytes) {
   return CLM_OK;
 }
 
-// Exact path: score chunks [nqb, ch] by the EPI_SCORE GEMM, radix top-k per chunk row,
-// merge the chunk lists. Any k <= 1024, any N.
-static int search_exact(clm_index* x, const u16* q16, const float* qinv, int64_t nq, int k, float* osc,
-                        int64_t* oix, hipStream_t st) {
+// The MFMA pass scores fp16 unit-rounded operands: |fp16-pass score - exact cosine| <= 2.05e-3
+// (each side's rounding moves a cosine by <= 2u, u = 2^-11, plus fp32 accumulation of <= 1024
+// products). Every row of the exact top-k therefore has an fp16-pass score within 2 x 2.05e-3 of
+// the fp16-pass k-th best; the candidates are taken that wide (plus slack) and re-scored exactly.
+constexpr float RESCORE_MARGIN = 5e-3f;
+constexpr int CAND_CAP = 2048;
+
+// Chunked scan: score chunks [nqb, ch] -- fp16 MFMA (EPI_SCORE GEMM) or exact fp64 cosines
+// (exact_scores) -- radix top-k per chunk row, merge of the chunk lists. Any k <= 1024, any N.
+static int search_scan(clm_index* x, bool exact, const u16* q16, const float* qinv, const float* q32,
+                       const double* qn, int64_t nq, int k, float* osc, int64_t* oix, hipStream_t st) {
   const int dim = (int)x->dim;
   const int64_t N = x->n;
   const size_t budget = (size_t)512 << 20;
@@ -1116,9 +1177,9 @@ static int search_exact(clm_index* x, const u16* q16, const float* qinv, int64_t
   const size_t o_sc = take((size_t)nqb * ch * 4);
   const size_t o_cs = take((size_t)nqb * std::max<int64_t>(nchunks, 1) * k * 4);
   const size_t o_ci = take((size_t)nqb * std::max<int64_t>(nchunks, 1) * k * 8);
-  int r = grow(&x->ws2, &x->ws2_bytes, off);
+  int r = grow(&x->ws3, &x->ws3_bytes, off);
   if (r) return r;
-  uint8_t* w = (uint8_t*)x->ws2;
+  uint8_t* w = (uint8_t*)x->ws3;
   float* sc = (float*)(w + o_sc);
   float* cs = (float*)(w + o_cs);
   int64_t* ci = (int64_t*)(w + o_ci);
@@ -1130,11 +1191,16 @@ static int search_exact(clm_index* x, const u16* q16, const float* qinv, int64_t
     }
     for (int64_t c = 0; c < nchunks; ++c) {
       const int64_t r0 = c * ch, rn = std::min(ch, N - r0);
-      GemmArgs ga{};
-      ga.A = q16 + q0 * dim; ga.lda = dim; ga.W = x->rows + r0 * dim; ga.ldw = dim;
-      ga.M = (int)nb; ga.N = (int)rn; ga.K = dim; ga.out = sc; ga.ldo = ch;
-      ga.rscale = qinv + q0; ga.cscale = x->inv + r0;
-      KCHK(gemm(false, EPI_SCORE, ga, st));
+      if (exact) {
+        const void* rp = x->rows32 ? (const void*)(x->rows32 + r0 * dim) : (const void*)(x->rows + r0 * dim);
+        KCHK(exact_scores(q32 + q0 * dim, qn + q0, nb, rp, !x->rows32, rn, dim, sc, ch, st));
+      } else {
+        GemmArgs ga{};
+        ga.A = q16 + q0 * dim; ga.lda = dim; ga.W = x->rows + r0 * dim; ga.ldw = dim;
+        ga.M = (int)nb; ga.N = (int)rn; ga.K = dim; ga.out = sc; ga.ldo = ch;
+        ga.rscale = qinv + q0; ga.cscale = x->inv + r0;
+        KCHK(gemm(false, EPI_SCORE, ga, st));
+      }
       if (nchunks == 1) {
         KCHK(topk_rows(sc, ch, nb, rn, k, x->offset + r0, osc + q0 * k, oix + q0 * k, k, st));
       } else {
@@ -1146,23 +1212,25 @@ static int search_exact(clm_index* x, const u16* q16, const float* qinv, int64_t
   return CLM_OK;
 }
 
-// Filtered path (large N, k <= 256), one pass over the index:
-//  1. theta[q] = k-th best score of q over a strided sample of S rows (exact path on the
-//     sample). The sample is a subset of the index, so theta[q] <= the true k-th best.
-//  2. the EPI_FILTER GEMM streams the whole index once (M-fastest tile order: each index
-//     tile is read once and shared by all query tiles) and appends every (score, row) with
-//     score >= theta[q] to q's candidate list (expected ~k*N/S = 256 entries, capacity CAP).
-//     Scores are bit-identical to the sample pass (same K order per dot product), so the
-//     candidates contain the exact top-k, ties included.
-//  3. per-query sort of the candidates (topk_merge) -> (score desc, index asc).
-//  Queries whose list overflowed CAP are redone on the exact path.
-constexpr int CAND_CAP = 2048;
-static int search_filtered(clm_index* x, const u16* q16, const float* qinv, int64_t nq, int k, int64_t S,
-                           float* osc, int64_t* oix, hipStream_t st) {
+// Bounded search (large N), per block of queries:
+//  1. theta[q] <= the fp16-pass k-th best score of q:
+//     sampled (k <= 256, N >= 4S): the k-th best over a strided sample of S rows -- a subset
+//       of the index, so never above the true fp16-pass k-th best;
+//     otherwise: the chunked fp16 scan's k-th best itself.
+//  2. the EPI_FILTER GEMM streams the whole index once (M-fastest tile order: each index tile
+//     is read once and shared by all query tiles) and appends every (score, row) with
+//     score >= theta[q] - RESCORE_MARGIN to q's candidate list (capacity CAND_CAP): a
+//     superset of the exact top-k.
+//  3. rescore_select: candidates within the margin of their k-th are re-scored exactly against
+//     the caller's rows, sorted (score desc, index asc), top k written.
+//  Lists that overflowed CAND_CAP are redone by the full exact scan.
+static int search_bounded(clm_index* x, bool sampled, int64_t S, const u16* q16, const float* qinv,
+                          const float* q32, const double* qn, int64_t nq, int k, float* osc, int64_t* oix,
+                          hipStream_t st) {
   const int dim = (int)x->dim;
   const int64_t N = x->n;
   int r;
-  if (x->samp_n != N || x->samp_S != S) {
+  if (sampled && (x->samp_n != N || x->samp_S != S)) {
     if (x->samp_cap < S) {
       if (x->samp) (void)hipFree(x->samp);
       if (x->samp_inv) (void)hipFree(x->samp_inv);
@@ -1177,16 +1245,25 @@ static int search_filtered(clm_index* x, const u16* q16, const float* qinv, int6
     x->samp_n = N;
     x->samp_S = S;
   }
-  // query block: its sample-score matrix (nqb x S fp32) is the workspace that bounds it; every
-  // block streams the whole index once through the filter GEMM, so fewer, larger blocks read
-  // the index fewer times (10 M x 512 fp16 = 10 GB per pass). $CLM_SEARCH_WS_MB overrides.
+  // query block: every block streams the whole index once through the filter GEMM, so fewer,
+  // larger blocks read the index fewer times (10 M x 512 fp16 = 10 GB per pass). The sampled
+  // path's block is bounded by its sample-score matrix (nqb x S fp32): at most $CLM_SEARCH_WS_MB
+  // (default 8192) and at most a quarter of the free HBM.
   static const int64_t ws_mb = getenv("CLM_SEARCH_WS_MB") ? atoll(getenv("CLM_SEARCH_WS_MB")) : 8192;
-  const int64_t nqb = std::min<int64_t>(nq, std::max<int64_t>(256, (ws_mb << 20) / ((int64_t)S * 4)));
+  int64_t nqb = std::min<int64_t>(nq, 4096);
+  if (sampled) {
+    size_t fr = 0, tot = 0;
+    int64_t cap_b = ws_mb << 20;
+    if (hipMemGetInfo(&fr, &tot) == hipSuccess) cap_b = std::min<int64_t>(cap_b, (int64_t)(fr / 4));
+    else (void)hipGetLastError();
+    nqb = std::min<int64_t>(nq, std::max<int64_t>(256, cap_b / ((int64_t)S * 4)));
+  }
   size_t off = 0;
   auto take = [&](size_t bytes) { size_t o = off; off = round_up(off + bytes, 256); return o; };
-  const size_t o_sc = take((size_t)nqb * S * 4);
+  const size_t o_sc = sampled ? take((size_t)nqb * S * 4) : 0;
   const size_t o_ts = take((size_t)nqb * k * 4);
   const size_t o_ti = take((size_t)nqb * k * 8);
+  const size_t o_th = take((size_t)nqb * 4);
   const size_t o_cnt = take((size_t)nqb * 4);
   const size_t o_cs = take((size_t)nqb * CAND_CAP * 4);
   const size_t o_ci = take((size_t)nqb * CAND_CAP * 8);
@@ -1195,47 +1272,60 @@ static int search_filtered(clm_index* x, const u16* q16, const float* qinv, int6
   float* sc = (float*)(w + o_sc);
   float* ts = (float*)(w + o_ts);
   int64_t* ti = (int64_t*)(w + o_ti);
+  float* th = (float*)(w + o_th);
   int* cnt = (int*)(w + o_cnt);
   float* cs = (float*)(w + o_cs);
   int64_t* ci = (int64_t*)(w + o_ci);
+  const void* xrows = x->rows32 ? (const void*)x->rows32 : (const void*)x->rows;
   std::vector<int> hcnt;
   std::vector<int64_t> overflow;
   for (int64_t q0 = 0; q0 < nq; q0 += nqb) {
     const int64_t nb = std::min(nqb, nq - q0);
-    GemmArgs ga{};
-    ga.A = q16 + q0 * dim; ga.lda = dim; ga.W = x->samp; ga.ldw = dim;
-    ga.M = (int)nb; ga.N = (int)S; ga.K = dim; ga.out = sc; ga.ldo = S;
-    ga.rscale = qinv + q0; ga.cscale = x->samp_inv;
-    KCHK(gemm(false, EPI_SCORE, ga, st));
-    KCHK(topk_rows(sc, S, nb, S, k, 0, ts, ti, k, st));
+    if (sampled) {
+      GemmArgs ga{};
+      ga.A = q16 + q0 * dim; ga.lda = dim; ga.W = x->samp; ga.ldw = dim;
+      ga.M = (int)nb; ga.N = (int)S; ga.K = dim; ga.out = sc; ga.ldo = S;
+      ga.rscale = qinv + q0; ga.cscale = x->samp_inv;
+      KCHK(gemm(false, EPI_SCORE, ga, st));
+      KCHK(topk_rows(sc, S, nb, S, k, 0, ts, ti, k, st));
+    } else {
+      if ((r = search_scan(x, false, q16 + q0 * dim, qinv + q0, nullptr, nullptr, nb, k, ts, ti, st))) return r;
+    }
+    KCHK(filter_thresholds(ts, k, nb, k, RESCORE_MARGIN, th, st));
     HIPCHK(hipMemsetAsync(cnt, 0, (size_t)nb * 4, st));
-    HIPCHK(hipMemsetAsync(ci, 0xFF, (size_t)nb * CAND_CAP * 8, st));
     GemmArgs gf{};
     gf.A = q16 + q0 * dim; gf.lda = dim; gf.W = x->rows; gf.ldw = dim;
     gf.M = (int)nb; gf.N = (int)N; gf.K = dim;
     gf.rscale = qinv + q0; gf.cscale = x->inv;
-    gf.theta = ts + (k - 1); gf.theta_ld = k;
+    gf.theta = th; gf.theta_ld = 1;
     gf.cnt = cnt; gf.cand_s = cs; gf.cand_i = ci; gf.cap = CAND_CAP; gf.base = x->offset;
     gf.m_fastest = 1;
     KCHK(gemm(false, EPI_FILTER, gf, st));
-    KCHK(topk_merge(cs, ci, nb, 1, CAND_CAP, k, osc + q0 * k, oix + q0 * k, st));
+    KCHK(rescore_select(cs, ci, cnt, CAND_CAP, q32 + q0 * dim, qn + q0, dim, xrows, !x->rows32, x->offset,
+                        RESCORE_MARGIN, nb, k, osc + q0 * k, oix + q0 * k, st));
     hcnt.resize(nb);
     HIPCHK(hipMemcpyAsync(hcnt.data(), cnt, (size_t)nb * 4, hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
     for (int64_t i = 0; i < nb; ++i)
       if (hcnt[i] > CAND_CAP) overflow.push_back(q0 + i);
   }
-  x->search_stats[0] += nq - (int64_t)overflow.size();
-  if (!overflow.empty()) {   // rare: a sample that under-estimates theta badly; redo exactly
+  x->search_stats[sampled ? 0 : 3] += nq - (int64_t)overflow.size();
+  if (!overflow.empty()) {   // rare: a candidate list beyond CAND_CAP (many near-ties); redo exactly
     x->search_stats[2] += (int64_t)overflow.size();
     for (int64_t qi : overflow) {
-      r = search_exact(x, q16 + qi * dim, qinv + qi, 1, k, osc + qi * k, oix + qi * k, st);
+      r = search_scan(x, true, nullptr, nullptr, q32 + qi * dim, qn + qi, 1, k, osc + qi * k, oix + qi * k, st);
       if (r) return r;
     }
   }
   return CLM_OK;
 }
 
+// Top-k by EXACT cosine (the fp32-rounded fp64 cosine of the caller's query and rows), order
+// (score desc, index asc). The reference ranks fp32 dot products of fp32-normalised rows
+// (search.py:36,68,93,96-99), i.e. the same scores to within its own fp32 summation error.
+//  * small problems (nq * N <= 2^24 dot products, or $CLM_SEARCH_FULL=1): the exact scan;
+//  * otherwise (or $CLM_SEARCH_BOUNDED=1) search_bounded, sampled when the index is large
+//    enough for sampling to pay ($CLM_SEARCH_EXACT=1 forces the chunked fp16 scan for step 1).
 int clm_index_search(clm_index* x, const void* q, int q_dtype, int64_t nq, int k, float* out_scores,
                      int64_t* out_idx, void* stream) {
   if (!x || nq < 0 || (nq > 0 && (!q || !out_scores || !out_idx))) return fail(CLM_E_ARG, "bad argument");
@@ -1254,6 +1344,8 @@ int clm_index_search(clm_index* x, const void* q, int q_dtype, int64_t nq, int k
   const size_t o_qsrc = q_dev ? 0 : take(q_src_bytes);
   const size_t o_q16 = take((size_t)nq * dim * 2);
   const size_t o_qinv = take((size_t)nq * 4);
+  const size_t o_q32 = (q_dtype == CLM_F32 && q_dev) ? 0 : take((size_t)nq * dim * 4);
+  const size_t o_qn = take((size_t)nq * 8);
   const size_t o_os = o_dev ? 0 : take((size_t)nq * k * 4);
   const size_t o_oi = o_dev ? 0 : take((size_t)nq * k * 8);
   int r = grow(&x->ws, &x->ws_bytes, off);
@@ -1266,26 +1358,38 @@ int clm_index_search(clm_index* x, const void* q, int q_dtype, int64_t nq, int k
   }
   u16* q16 = (u16*)(ws + o_q16);
   float* qinv = (float*)(ws + o_qinv);
-  // inverse norms of the SOURCE rows (reference normalises the fp32 query, search.py:93)
-  KCHK(rows_to_f16(qsrc, q_dtype == CLM_F32 ? 0 : 1, nq, dim, q16, qinv, st, 1));
+  const float* q32 = (const float*)qsrc;
+  if (!(q_dtype == CLM_F32 && q_dev)) {
+    float* t = (float*)(ws + o_q32);
+    if (q_dtype == CLM_F32) HIPCHK(hipMemcpyAsync(t, qsrc, (size_t)nq * dim * 4, hipMemcpyDeviceToDevice, st));
+    else KCHK(f16_to_f32_rows((const u16*)qsrc, nq, dim, t, st));
+    q32 = t;
+  }
+  double* qn = (double*)(ws + o_qn);
+  KCHK(query_norms(q32, nq, dim, qn, st));
+  // fp16 operands of the MFMA pass: queries normalised, then rounded
+  KCHK(rows_to_f16(qsrc, q_dtype == CLM_F32 ? 0 : 1, nq, dim, q16, qinv, st, 2));
   float* osc = o_dev ? out_scores : (float*)(ws + o_os);
   int64_t* oix = o_dev ? out_idx : (int64_t*)(ws + o_oi);
-  // filtered single-pass path when the index is large enough for sampling to pay
-  int64_t S = round_up(std::max<int64_t>(8192, (int64_t)k * N / 256), 256);
-  const char* env = getenv("CLM_SEARCH_EXACT");
-  const bool filtered = !(env && atoi(env)) && k <= 256 && N >= 4 * S && S <= (1 << 18);
-  if (filtered) r = search_filtered(x, q16, qinv, nq, k, S, osc, oix, st);
-  else {
-    r = search_exact(x, q16, qinv, nq, k, osc, oix, st);
+  const char* e_full = getenv("CLM_SEARCH_FULL");
+  const char* e_exact = getenv("CLM_SEARCH_EXACT");
+  const char* e_bounded = getenv("CLM_SEARCH_BOUNDED");   // tests: bounded search at any size
+  const bool force_bounded = e_bounded && atoi(e_bounded) && N > 0;
+  if ((e_full && atoi(e_full)) || N == 0 || (!force_bounded && (double)nq * (double)N <= (double)(1 << 24))) {
+    r = search_scan(x, true, q16, qinv, q32, qn, nq, k, osc, oix, st);
     x->search_stats[1] += nq;
+  } else {
+    const int64_t S = round_up(std::max<int64_t>(8192, (int64_t)k * N / 256), 256);
+    const bool sampled = !(e_exact && atoi(e_exact)) && k <= 256 && N >= 4 * S && S <= (1 << 18);
+    r = search_bounded(x, sampled, S, q16, qinv, q32, qn, nq, k, osc, oix, st);
   }
   if (r) return r;
   if (!o_dev) {
     HIPCHK(hipMemcpyAsync(out_scores, osc, (size_t)nq * k * 4, hipMemcpyDeviceToHost, st));
     HIPCHK(hipMemcpyAsync(out_idx, oix, (size_t)nq * k * 8, hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
-  } else if (!q_dev) {
-    HIPCHK(hipStreamSynchronize(st));
+  } else {
+    HIPCHK(hipStreamSynchronize(st));   // workspaces are reused by the next call
   }
   return CLM_OK;
 }
@@ -1293,29 +1397,34 @@ int clm_index_search(clm_index* x, const void* q, int q_dtype, int64_t nq, int k
 int clm_index_stats(const clm_index* x, int64_t* filtered, int64_t* exact, int64_t* overflow) {
   if (!x) return fail(CLM_E_ARG, "null index");
   if (filtered) *filtered = x->search_stats[0];
-  if (exact) *exact = x->search_stats[1];
+  if (exact) *exact = x->search_stats[1] + x->search_stats[3];
   if (overflow) *overflow = x->search_stats[2];
   return CLM_OK;
 }
 
+int clm_index_stats2(const clm_index* x, int64_t* out, int n) {
+  if (!x || !out || n < 0) return fail(CLM_E_ARG, "bad argument");
+  const int64_t v[4] = {x->search_stats[0], x->search_stats[3], x->search_stats[1], x->search_stats[2]};
+  for (int i = 0; i < n && i < 4; ++i) out[i] = v[i];
+  return CLM_OK;
+}
+
+// similarity.cosine_similarity (similarity.py:10-33): every score exact (fp32-rounded fp64 cosine)
 int clm_cosine_scores(int hip_device, const float* q, int64_t nq, const float* c, int64_t n, int dim, float* out,
                       void* stream) {
-  if (nq < 0 || n < 0 || dim <= 0 || dim % 64 || (nq * n > 0 && (!q || !c || !out)))
-    return fail(CLM_E_ARG, "bad argument (dim must be a multiple of 64)");
+  if (nq < 0 || n < 0 || dim <= 0 || (nq * n > 0 && (!q || !c || !out)))
+    return fail(CLM_E_ARG, "bad argument");
   if (nq == 0 || n == 0) return CLM_OK;
   DeviceGuard g(hip_device);
   hipStream_t st = (hipStream_t)stream;
   const bool qd = is_device_ptr(q), cd = is_device_ptr(c), od = is_device_ptr(out);
-  size_t bytes = (size_t)(nq + n) * dim * 2 + (size_t)(nq + n) * 4 + (qd ? 0 : (size_t)nq * dim * 4) +
-                 (cd ? 0 : (size_t)n * dim * 4) + (od ? 0 : (size_t)nq * n * 4) + 1024;
+  size_t bytes = (size_t)nq * 8 + (qd ? 0 : (size_t)nq * dim * 4) + (cd ? 0 : (size_t)n * dim * 4) +
+                 (od ? 0 : (size_t)nq * n * 4) + 1024;
   uint8_t* w = nullptr;
   if (hipMalloc(&w, bytes) != hipSuccess) { (void)hipGetLastError(); return fail(CLM_E_OOM, "workspace"); }
   size_t off = 0;
   auto take = [&](size_t b) { size_t o = off; off = round_up(off + b, 256); return w + o; };
-  u16* q16 = (u16*)take((size_t)nq * dim * 2);
-  u16* c16 = (u16*)take((size_t)n * dim * 2);
-  float* qi = (float*)take((size_t)nq * 4);
-  float* cinv = (float*)take((size_t)n * 4);
+  double* qn = (double*)take((size_t)nq * 8);
   const float* qs = q;
   const float* cs = c;
   float* os = out;
@@ -1324,14 +1433,8 @@ int clm_cosine_scores(int hip_device, const float* q, int64_t nq, const float* c
   if (!qd) { float* t = (float*)take((size_t)nq * dim * 4); e = hipMemcpyAsync(t, q, (size_t)nq * dim * 4, hipMemcpyHostToDevice, st); qs = t; }
   if (e == hipSuccess && !cd) { float* t = (float*)take((size_t)n * dim * 4); e = hipMemcpyAsync(t, c, (size_t)n * dim * 4, hipMemcpyHostToDevice, st); cs = t; }
   if (!od) os = (float*)take((size_t)nq * n * 4);
-  if (e == hipSuccess) e = rows_to_f16(qs, 0, nq, dim, q16, qi, st, 1);
-  if (e == hipSuccess) e = rows_to_f16(cs, 0, n, dim, c16, cinv, st, 1);
-  if (e == hipSuccess) {
-    GemmArgs ga{};
-    ga.A = q16; ga.lda = dim; ga.W = c16; ga.ldw = dim; ga.M = (int)nq; ga.N = (int)n; ga.K = dim;
-    ga.out = os; ga.ldo = n; ga.rscale = qi; ga.cscale = cinv;
-    e = gemm(false, EPI_SCORE, ga, st);
-  }
+  if (e == hipSuccess) e = query_norms(qs, nq, dim, qn, st);
+  if (e == hipSuccess) e = exact_scores(qs, qn, nq, cs, false, n, dim, os, n, st);
   if (e == hipSuccess && !od) e = hipMemcpyAsync(out, os, (size_t)nq * n * 4, hipMemcpyDeviceToHost, st);
   if (e == hipSuccess) e = hipStreamSynchronize(st);
   if (e != hipSuccess) rc = fail(CLM_E_HIP, std::string("cosine_scores: ") + hipGetErrorString(e));

@@ -476,14 +476,25 @@ __global__ __launch_bounds__(256) void rows_to_f16_kernel(const void* src, int s
   const int lane = threadIdx.x & 63;
   const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= n) return;
+  auto load = [&](int e) {
+    return src_dtype == 0 ? ((const float*)src)[row * dim + e] : f16_to_f32(((const u16*)src)[row * dim + e]);
+  };
+  // norm_src 2: round v / ||v|| (unit rows: no fp16 overflow, no subnormal loss of tiny rows)
+  float scale = 1.f;
+  if (norm_src == 2) {
+    float s0 = 0.f;
+    for (int e = lane; e < dim; e += 64) {
+      const float v = load(e);
+      s0 += v * v;
+    }
+    scale = 1.0f / sqrtf(wave_sum(s0));
+  }
   float s = 0.f;
   for (int e = lane; e < dim; e += 64) {
-    float v;
-    if (src_dtype == 0) v = ((const float*)src)[row * dim + e];
-    else v = f16_to_f32(((const u16*)src)[row * dim + e]);
+    const float v = load(e) * scale;
     const u16 hv = f32_to_f16(v);
     dst[row * dim + e] = hv;
-    const float r = norm_src ? v : f16_to_f32(hv);
+    const float r = norm_src == 1 ? v : f16_to_f32(hv);
     s += r * r;
   }
   s = wave_sum(s);

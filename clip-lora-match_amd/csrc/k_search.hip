@@ -183,6 +183,143 @@ __global__ __launch_bounds__(NT) void topk_rows_kernel(const float* S, int64_t l
   }
 }
 
+// ---- exact (fp64) cosine re-scoring ---------------------------------------------------------
+// The reference ranks fp32 rows by fp32 dot products of fp32-normalised vectors
+// (search.py:36,68,93,96; similarity.py:30-32). The MFMA pass ranks fp16-rounded operands, so
+// its scores are within MARGIN/2 of the exact cosine; these kernels recompute the cosine of
+// the caller's own fp32 (or fp16) rows in fp64 -- fp32 x fp32 products are exact in fp64 --
+// and round once to fp32. Every kernel goes through cos_wave, with one fixed element -> lane
+// mapping and reduction order, so a (query, row) pair scores bit-identically on every path.
+template <typename R>
+__device__ __forceinline__ float row_elem(const R* r, int64_t e) {
+  if constexpr (sizeof(R) == 2) return f16_to_f32(r[e]);
+  else return r[e];
+}
+
+// lane-partial fp64 sums over elements e = lane + 64 i, then one xor-tree over the wave
+template <typename R>
+__device__ __forceinline__ void dot_wave(const float* q, const R* r, int dim, int lane, double& dot, double& rr) {
+  double a = 0.0, b = 0.0;
+  for (int e = lane; e < dim; e += 64) {
+    const double rv = (double)row_elem(r, e);
+    a = fma((double)q[e], rv, a);
+    b = fma(rv, rv, b);
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    a += __shfl_xor(a, o, 64);
+    b += __shfl_xor(b, o, 64);
+  }
+  dot = a;
+  rr = b;
+}
+
+__device__ __forceinline__ float cos_from(double dot, double qn, double rr) {
+  return (float)(dot / (qn * sqrt(rr)));
+}
+
+// qn[q] = ||q||_2 in fp64 (same lane mapping as dot_wave)
+__global__ __launch_bounds__(256) void qnorm_kernel(const float* q, int64_t nq, int dim, double* qn) {
+  const int lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= nq) return;
+  double d, s;
+  dot_wave(q + row * dim, q + row * dim, dim, lane, d, s);
+  if (lane == 0) qn[row] = sqrt(s);
+}
+
+// out[qi, j] = cos(q[qi], rows[r0 + j]) for j < rn, qi < nq: one wave per row, queries looped
+template <typename R>
+__global__ __launch_bounds__(256) void exact_scores_kernel(const float* q, const double* qn, int64_t nq,
+                                                           const R* rows, int64_t rn, int dim, float* out,
+                                                           int64_t ldo) {
+  const int lane = threadIdx.x & 63;
+  const int64_t j = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (j >= rn) return;
+  const R* r = rows + j * dim;
+  for (int64_t qi = 0; qi < nq; ++qi) {
+    double d, rr;
+    dot_wave(q + qi * dim, r, dim, lane, d, rr);
+    if (lane == 0) out[qi * ldo + j] = cos_from(d, qn[qi], rr);
+  }
+}
+
+// Per query (one 1024-thread workgroup): sort the filter candidates (fp16-pass score, global
+// index) desc, keep those within `margin` of the k-th -- a superset of the exact top-k, since
+// |fp16-pass score - exact cosine| <= margin / 2 -- re-score them exactly and emit the top k
+// by (exact score desc, index asc). cnt[q] > cap marks an incomplete list: nothing is written
+// for that query (the host redoes it with the full exact scan).
+template <typename R>
+__global__ __launch_bounds__(NT) void rescore_select_kernel(const float* cs, const int64_t* ci, const int* cnt,
+                                                            int cap, const float* q, const double* qn, int dim,
+                                                            const R* rows, int64_t offset, float margin, int k,
+                                                            float* os, int64_t* oi) {
+  __shared__ uint64_t keys[SORT_MAX];
+  __shared__ int s_m;
+  const int64_t row = blockIdx.x;
+  const int c = cnt[row];
+  if (c > cap) return;
+  int n2 = 1;
+  while (n2 < c) n2 <<= 1;
+  for (int j = threadIdx.x; j < n2; j += NT) {
+    uint64_t v = 0;
+    if (j < c) {
+      const int64_t ix = ci[row * cap + j];
+      v = ((uint64_t)fkey(cs[row * cap + j]) << 32) | (uint64_t)(0xFFFFFFFFu - (uint32_t)ix);
+    }
+    keys[j] = v;
+  }
+  __syncthreads();
+  if (n2 > 1) bitonic_desc(keys, n2);
+  const float thr = c >= k ? kfloat((uint32_t)(keys[k - 1] >> 32)) - margin : -INFINITY;
+  if (threadIdx.x == 0) s_m = c;
+  __syncthreads();
+  for (int j = threadIdx.x; j < c; j += NT)
+    if (kfloat((uint32_t)(keys[j] >> 32)) < thr && (j == 0 || kfloat((uint32_t)(keys[j - 1] >> 32)) >= thr))
+      s_m = j;
+  __syncthreads();
+  const int m = s_m;
+  // exact scores of the m survivors, one wave per candidate, written back in place
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const float* qr = q + row * dim;
+  const double qnr = qn[row];
+  for (int j = wid; j < m; j += NT / 64) {
+    const uint32_t low = (uint32_t)(keys[j] & 0xFFFFFFFFu);
+    const int64_t gix = (int64_t)(0xFFFFFFFFu - low);
+    double d, rr;
+    dot_wave(qr, rows + (gix - offset) * dim, dim, lane, d, rr);
+    const float sc = cos_from(d, qnr, rr);
+    if (lane == 0) keys[j] = ((uint64_t)fkey(sc) << 32) | low;
+  }
+  __syncthreads();
+  int m2 = 1;
+  while (m2 < m) m2 <<= 1;
+  for (int j = m + threadIdx.x; j < m2; j += NT) keys[j] = 0;
+  __syncthreads();
+  if (m2 > 1) bitonic_desc(keys, m2);
+  for (int j = threadIdx.x; j < k; j += NT) {
+    if (j < m) {
+      const uint64_t v = keys[j];
+      os[row * k + j] = kfloat((uint32_t)(v >> 32));
+      oi[row * k + j] = (int64_t)(0xFFFFFFFFu - (uint32_t)(v & 0xFFFFFFFFu));
+    } else {
+      os[row * k + j] = -INFINITY;
+      oi[row * k + j] = -1;
+    }
+  }
+}
+
+// filter threshold: th[q] = fp16-pass k-th score of q (ts[q * ld + k - 1]) - margin
+__global__ void theta_kernel(const float* ts, int64_t ld, int64_t nq, int k, float margin, float* th) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < nq) th[i] = ts[i * ld + k - 1] - margin;
+}
+
+__global__ void upcast_f16_kernel(const u16* src, int64_t total, float* dst) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x)
+    dst[i] = f16_to_f32(src[i]);
+}
+
 __global__ __launch_bounds__(NT) void topk_merge_kernel(const float* in_s, const int64_t* in_i, int n_in,
                                                         int k, float* os, int64_t* oi) {
   __shared__ uint64_t cand[SORT_MAX];
@@ -223,6 +360,51 @@ hipError_t topk_merge(const float* in_s, const int64_t* in_i, int64_t nq, int pa
   const int n_in = parts * k_in;
   if (n_in > SORT_MAX || k < 1 || k > 1024) return hipErrorInvalidValue;
   topk_merge_kernel<<<(unsigned)nq, NT, 0, s>>>(in_s, in_i, n_in, k, out_s, out_i);
+  return hipGetLastError();
+}
+
+hipError_t query_norms(const float* q, int64_t nq, int dim, double* qn, hipStream_t s) {
+  if (nq <= 0) return hipSuccess;
+  qnorm_kernel<<<(unsigned)((nq + 3) / 4), 256, 0, s>>>(q, nq, dim, qn);
+  return hipGetLastError();
+}
+
+hipError_t exact_scores(const float* q, const double* qn, int64_t nq, const void* rows, bool rows_f16, int64_t rn,
+                        int dim, float* out, int64_t ldo, hipStream_t s) {
+  if (nq <= 0 || rn <= 0) return hipSuccess;
+  const unsigned grid = (unsigned)((rn + 3) / 4);
+  if (rows_f16)
+    exact_scores_kernel<u16><<<grid, 256, 0, s>>>(q, qn, nq, (const u16*)rows, rn, dim, out, ldo);
+  else
+    exact_scores_kernel<float><<<grid, 256, 0, s>>>(q, qn, nq, (const float*)rows, rn, dim, out, ldo);
+  return hipGetLastError();
+}
+
+hipError_t rescore_select(const float* cand_s, const int64_t* cand_i, const int* cnt, int cap, const float* q,
+                          const double* qn, int dim, const void* rows, bool rows_f16, int64_t offset, float margin,
+                          int64_t nq, int k, float* out_s, int64_t* out_i, hipStream_t s) {
+  if (nq <= 0) return hipSuccess;
+  if (cap > SORT_MAX || k < 1 || k > 1024) return hipErrorInvalidValue;
+  if (rows_f16)
+    rescore_select_kernel<u16><<<(unsigned)nq, NT, 0, s>>>(cand_s, cand_i, cnt, cap, q, qn, dim, (const u16*)rows,
+                                                           offset, margin, k, out_s, out_i);
+  else
+    rescore_select_kernel<float><<<(unsigned)nq, NT, 0, s>>>(cand_s, cand_i, cnt, cap, q, qn, dim,
+                                                             (const float*)rows, offset, margin, k, out_s, out_i);
+  return hipGetLastError();
+}
+
+hipError_t filter_thresholds(const float* ts, int64_t ld, int64_t nq, int k, float margin, float* th, hipStream_t s) {
+  if (nq <= 0) return hipSuccess;
+  theta_kernel<<<(unsigned)((nq + 255) / 256), 256, 0, s>>>(ts, ld, nq, k, margin, th);
+  return hipGetLastError();
+}
+
+hipError_t f16_to_f32_rows(const u16* src, int64_t n, int dim, float* dst, hipStream_t s) {
+  const int64_t total = n * dim;
+  if (total <= 0) return hipSuccess;
+  const int blocks = (int)std::min<int64_t>((total + 255) / 256, 4096);
+  upcast_f16_kernel<<<blocks, 256, 0, s>>>(src, total, dst);
   return hipGetLastError();
 }
 

@@ -89,7 +89,8 @@ hipError_t attention(bool bf16, bool causal, const u16* qkv, int64_t ldq, u16* o
 
 // ----------------------------------------------------------- search --------
 // rows f32|f16 [n, dim] -> fp16 dst + fp32 inverse norms of the fp16-rounded rows
-// (norm_src = 0) or of the source rows (norm_src = 1)
+// (norm_src = 0) or of the source rows (norm_src = 1); norm_src = 2: dst = fp16(v / ||v||)
+// and the inverse norms of those rounded unit rows
 hipError_t rows_to_f16(const void* src, int src_dtype, int64_t n, int dim, u16* dst,
                        float* inv_norm, hipStream_t s, int norm_src);
 // per-row top-k over scores [nq, C] (row stride lds): out sorted by (score desc,
@@ -106,5 +107,21 @@ hipError_t fuse_rows(const float* a, float wa, const float* b, float wb, int64_t
 hipError_t sample_rows(const u16* rows, const float* inv, int64_t n, int dim, int64_t S, u16* out_rows,
                        float* out_inv, hipStream_t s);
 hipError_t f32_to_f16_rows(const float* src, int64_t n, int dim, u16* dst, hipStream_t s);
+hipError_t f16_to_f32_rows(const u16* src, int64_t n, int dim, float* dst, hipStream_t s);
+
+// exact (fp64) cosine re-scoring (k_search.hip): every path scores a (query, row) pair through
+// one device routine, so the exact scores are bit-identical across paths
+hipError_t query_norms(const float* q, int64_t nq, int dim, double* qn, hipStream_t s);
+// out[qi, j] = fp32(cos64(q[qi], rows[j])), rows f32 or f16 [rn, dim]
+hipError_t exact_scores(const float* q, const double* qn, int64_t nq, const void* rows, bool rows_f16, int64_t rn,
+                        int dim, float* out, int64_t ldo, hipStream_t s);
+// per query: candidates (fp16-pass score, global index) [nq, cap] with counts cnt[nq] -> keep
+// those within `margin` of the k-th, re-score exactly, emit top k by (score desc, index asc);
+// queries with cnt > cap are left untouched
+hipError_t rescore_select(const float* cand_s, const int64_t* cand_i, const int* cnt, int cap, const float* q,
+                          const double* qn, int dim, const void* rows, bool rows_f16, int64_t offset, float margin,
+                          int64_t nq, int k, float* out_s, int64_t* out_i, hipStream_t s);
+// th[q] = ts[q * ld + k - 1] - margin
+hipError_t filter_thresholds(const float* ts, int64_t ld, int64_t nq, int k, float margin, float* th, hipStream_t s);
 
 }  // namespace clm

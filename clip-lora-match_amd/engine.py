@@ -70,6 +70,16 @@ class ClipLoraModel:
         C.check(C.lib().clm_finalize(self._ctx), "clm_finalize")
         return self
 
+    def attach_lora(self, r: int, alpha: float, targets, tensors: Dict[str, np.ndarray]) -> "ClipLoraModel":
+        """Attach (or replace) LoRA adapters on THIS model's weights, in place -- what PEFT's
+        get_peft_model does to the CLIPModel it is given (models/lora_adapter.py:46-56)."""
+        cfg = self.cfg.with_lora(r, alpha, targets)
+        C.check(C.lib().clm_set_lora(self._ctx, int(cfg.lora_r), float(cfg.lora_alpha), int(cfg.lora_mask)),
+                "clm_set_lora")
+        self.cfg = cfg
+        self.load_tensors(tensors)
+        return self.finalize()
+
     def set_lora_enabled(self, enabled: bool) -> None:
         C.check(C.lib().clm_set_lora_enabled(self._ctx, int(bool(enabled))), "clm_set_lora_enabled")
 

@@ -66,7 +66,8 @@ def rebuild_index(model, processor, descriptions: Sequence, image_paths: Sequenc
                   group=None) -> torch.Tensor:
     """rebuild_index.py:28-115: embed every item (its description by default, as the reference
     does; its image with from_images=True), save the .pt index, return the [N, D] CPU rows.
-    Under torch.distributed only rank 0 writes the file. No items: nothing is written (:54-56)."""
+    Under torch.distributed only rank 0 writes the file (to a temporary name, renamed into
+    place), and every rank returns after it exists. No items: nothing is written (:54-56)."""
     if len(descriptions) != len(image_paths):
         raise ValueError(f"{len(descriptions)} descriptions vs {len(image_paths)} image paths")
     if len(descriptions) == 0:
@@ -76,12 +77,16 @@ def rebuild_index(model, processor, descriptions: Sequence, image_paths: Sequenc
     else:
         rows = encode_items(model, processor, texts=list(descriptions), batch_size=batch_size, group=group)
     rows = rows.cpu()
-    rank0 = not (dist.is_available() and dist.is_initialized()) or dist.get_rank(group) == 0
-    if rank0:
+    distributed = dist.is_available() and dist.is_initialized()
+    if not distributed or dist.get_rank(group) == 0:
         index_path = Path(index_path)
         index_path.parent.mkdir(parents=True, exist_ok=True)
         texts = [d if isinstance(d, str) else "" for d in descriptions]
-        torch.save({"embeddings": rows, "image_paths": [str(p) for p in image_paths], "texts": texts}, index_path)
+        tmp = index_path.with_name(index_path.name + ".tmp")
+        torch.save({"embeddings": rows, "image_paths": [str(p) for p in image_paths], "texts": texts}, tmp)
+        tmp.replace(index_path)   # readers never see a partial file
+    if distributed:
+        dist.barrier(group)       # every rank returns after the file is in place
     return rows
 
 

@@ -7,7 +7,9 @@
                                               Linear whose name ends in a target
                                               (PEFT suffix matching: both towers)
 PEFT initialises lora_B = 0, so a freshly attached adapter is an exact no-op;
-init="synthetic" attaches the deterministic non-zero adapter instead.
+init="synthetic" attaches the deterministic non-zero adapter instead. The adapters
+are attached to the given model's own weights, in place (clm_set_lora on its
+context), as get_peft_model does.
 """
 from __future__ import annotations
 
@@ -15,6 +17,7 @@ from dataclasses import dataclass, field
 from pathlib import Path
 from typing import List, Union
 
+import numpy as np
 import yaml
 
 from . import weights as W
@@ -54,25 +57,22 @@ def create_lora_config(config_path: Union[str, Path] = "config/lora_config.yaml"
 
 
 def attach_lora_to_clip(model: ClipLoraModel, lora_config: LoraConfig, init: str = "peft",
-                        state_dict=None, seed: int = 1) -> ClipLoraModel:
-    """Return a new GPU model with adapters of `lora_config` attached.
-    state_dict: the base weights (numpy, by transformers name); defaults to the
-    deterministic synthetic weights of model.cfg."""
+                        seed: int = 1) -> ClipLoraModel:
+    """Wrap `model` -- its own loaded weights -- with adapters of `lora_config` on every Linear
+    whose name ends in a target (lora_adapter.py:46-56; PEFT matches by suffix: both towers).
+    Like get_peft_model the model is modified in place and returned.
+    init="peft": lora_B = 0 (PEFT's initialisation: an exact no-op until trained weights are
+    loaded); init="synthetic": the deterministic non-zero adapter."""
     cfg = model.cfg.with_lora(lora_config.r, lora_config.lora_alpha, lora_config.target_modules)
-    sd = state_dict if state_dict is not None else W.synthetic_state_dict(model.cfg.with_lora(0, 0, ()), 0)
     if init == "synthetic":
         lora = W.synthetic_lora(cfg, seed)
     elif init == "peft":
         lora = {k: (v * 0.0 if ".lora_B." in k else v) for k, v in W.synthetic_lora(cfg, seed).items()}
     else:
         raise ValueError("init must be 'peft' or 'synthetic'")
-    out = ClipLoraModel(cfg, device=model.device, compute_dtype=model.compute_dtype, lora_mode=model.lora_mode,
-                        max_batch=model.max_batch)
-    out.load_tensors(sd)
-    out.load_tensors(lora)
-    out.finalize()
+    model.attach_lora(cfg.lora_r, cfg.lora_alpha, cfg.lora_targets, lora)
     trainable = W.lora_param_count(cfg)
-    total = sum(int(v.size) for v in sd.values()) + trainable
+    total = sum(int(np.prod(s)) for s in W.state_dict_shapes(cfg).values()) + trainable
     print(f"trainable params: {trainable:,d} || all params: {total:,d} || "
           f"trainable%: {100.0 * trainable / total:.4f}")
-    return out
+    return model

@@ -9,11 +9,11 @@ the host by transformers' own CLIPImageProcessor when importable, else by a
 PIL bicubic shortest-edge resize + centre crop, and handed over as float32
 pixel_values.
 
-Text side: the CLIP BPE vocabulary is not shipped in this environment
-(SURVEY §8(c)); a local tokenizer directory (vocab.json + merges.txt) can be
-given via `tokenizer_dir` / $CLM_TOKENIZER_DIR, otherwise callers pass token
-ids directly (list[int] / [n, L] tensor), BOS ... EOS padded with EOS exactly as
-CLIPTokenizer(padding=True) produces.
+Text side: tokenizer.ClipBPETokenizer (CLIP byte-level BPE, host-side) over a local
+vocab.json + merges.txt given via `tokenizer_dir` / $CLM_TOKENIZER_DIR (the CLIP
+vocabulary is not shipped in this environment); without one, callers
+pass token ids directly (list[int] / [n, L] tensor), BOS ... EOS padded with EOS
+exactly as CLIPTokenizer(padding=True) produces.
 """
 from __future__ import annotations
 
@@ -43,8 +43,8 @@ class ClipProcessor:
         self.tokenizer = None
         tdir = tokenizer_dir or os.environ.get("CLM_TOKENIZER_DIR")
         if tdir and Path(tdir, "vocab.json").exists() and Path(tdir, "merges.txt").exists():
-            from transformers import CLIPTokenizer
-            self.tokenizer = CLIPTokenizer(str(Path(tdir, "vocab.json")), str(Path(tdir, "merges.txt")))
+            from .tokenizer import ClipBPETokenizer
+            self.tokenizer = ClipBPETokenizer.from_dir(tdir, model_max_length=cfg.max_pos)
 
     # ------------------------------------------------------------- images --
     @staticmethod
@@ -122,7 +122,10 @@ class ClipProcessor:
                     "the CLIP BPE vocabulary is not available offline; set CLM_TOKENIZER_DIR to a directory "
                     "with vocab.json + merges.txt, or pass token ids")
             enc = self.tokenizer(texts, padding=True, truncation=True, max_length=L, return_tensors="pt")
-            return enc["input_ids"].to(torch.int32)
+            ids = enc["input_ids"].to(torch.int32)
+            if (ids >= self.cfg.vocab).any():
+                raise ValueError(f"tokenizer produced ids >= the model's vocabulary size {self.cfg.vocab}")
+            return ids
         rows: List[List[int]] = [list(text)] if (text and isinstance(text[0], (int, np.integer))) else \
             [list(r) for r in text]
         rows = [r[:L] if len(r) <= L else r[:L - 1] + [eos] for r in rows]

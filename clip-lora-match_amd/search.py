@@ -6,13 +6,15 @@ exact top-k kernels.
   TextSearchIndex.__init__           search.py:24-68  (key variants :41-56, re-normalise :68)
   .search_with_embedding             search.py:70-115 (shape checks :80-90, safe metadata :103-105)
   .search_by_text / .search_by_image search.py:117-151
-New: .append / .save keep the index resident with O(1)
-append instead of FinderService's torch.cat + full re-save per report
-(finder_service.py:93-103,172-185), and .search_batch serves many queries per
-launch.
+New: .append / .save keep the index resident with amortised
+O(1) append instead of FinderService's torch.cat + full re-save per report
+(finder_service.py:93-103,172-185; the report flow itself is finder.py), and
+.search_batch serves many queries per launch.
 
-Top-k order is (score desc, index asc); CPU torch.topk leaves exact ties in
-arbitrary order (SURVEY §7 hard part 2).
+Scores are the exact cosines of the stored fp32 rows (fp64 arithmetic, rounded
+once): the fp16 MFMA pass only bounds the candidates (clm_index_search). Top-k
+order is (score desc, index asc); CPU torch.topk leaves exact ties in arbitrary
+order (SURVEY §7 hard part 2).
 """
 from __future__ import annotations
 
@@ -103,10 +105,13 @@ class CosineIndex:
         return s, i
 
     def stats(self) -> dict:
-        """queries served by the single-pass filtered path / the exact path / overflow re-runs"""
-        f, e, o = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
-        C.check(C.lib().clm_index_stats(self._h, ctypes.byref(f), ctypes.byref(e), ctypes.byref(o)))
-        return {"filtered": f.value, "exact": e.value, "overflow": o.value}
+        """queries served by the sampled single-pass bounded search (`filtered`), the bounded
+        search with a chunked fp16 scan as its first step (`scan_bounded`), the full exact
+        scan (`full_exact`), their sum `exact`, and overflow re-runs (include/clm.h)"""
+        v = (ctypes.c_int64 * 4)()
+        C.check(C.lib().clm_index_stats2(self._h, v, 4))
+        return {"filtered": v[0], "scan_bounded": v[1], "full_exact": v[2], "exact": v[1] + v[2],
+                "overflow": v[3]}
 
     def close(self) -> None:
         if getattr(self, "_h", None):
@@ -159,11 +164,24 @@ class TextSearchIndex:
         self.num_items, self.dim = self.embeddings.shape
         print(f"[TextSearchIndex] Loaded {self.num_items} items with dim={self.dim}")
 
-        # Pastikan normalized (search.py:68) -- fp32 on the host, as the reference does
+        # Pastikan normalized (search.py:68) -- fp32 on the host, as the reference does; the GPU
+        # index keeps these fp32 rows for its exact re-score
         self.embeddings = self.embeddings / self.embeddings.norm(dim=-1, keepdim=True)
         self._gpu = CosineIndex(self.dim, capacity=max(self.num_items, 1024), device=device)
         if self.num_items:
             self._gpu.append(self.embeddings)
+
+    # host mirror of the rows: a capacity-doubling buffer, so append is amortised O(1) (the
+    # reference's FinderService torch.cat's the whole index per report, finder_service.py:180)
+    @property
+    def embeddings(self) -> torch.Tensor:
+        return self._host[: self._n]
+
+    @embeddings.setter
+    def embeddings(self, value) -> None:
+        t = torch.as_tensor(value).float().cpu()
+        self._host = t.contiguous() if t.dim() == 2 else t
+        self._n = self._host.shape[0] if self._host.dim() >= 1 else 0
 
     # --------------------------------------------------------------- search --
     def search_batch(self, queries, top_k: int = 5) -> Tuple[torch.Tensor, torch.Tensor]:
@@ -206,20 +224,33 @@ class TextSearchIndex:
 
     # ------------------------------------------------------- resident append --
     def append(self, embeddings, image_paths: Sequence[str] = (), texts: Sequence[str] = ()) -> None:
+        """Add rows (re-normalised in fp32, as finder_service.py:169 does) and their metadata:
+        amortised O(1) per row on the host and in HBM."""
         e = torch.as_tensor(embeddings).float().cpu()
         if e.dim() == 1:
             e = e.unsqueeze(0)
-        if e.shape[1] != self.dim:
-            raise ValueError(f"embedding dim {e.shape[1]} != index dim {self.dim}")
+        if e.dim() != 2 or e.shape[1] != self.dim:
+            raise ValueError(f"embedding dim {e.shape[-1]} != index dim {self.dim}")
         e = e / e.norm(dim=-1, keepdim=True)
+        n_new = self._n + e.shape[0]
+        if n_new > self._host.shape[0]:
+            cap = max(n_new, 2 * self._host.shape[0], 1024)
+            buf = torch.empty((cap, self.dim), dtype=torch.float32)
+            buf[: self._n] = self._host[: self._n]
+            self._host = buf
+        self._host[self._n: n_new] = e
         self._gpu.append(e)
-        self.embeddings = torch.cat([self.embeddings, e], dim=0)
+        self._n = n_new
         self.image_paths.extend(image_paths)
         self.texts.extend(texts)
-        self.num_items = self.embeddings.shape[0]
+        self.num_items = n_new
 
     def save(self, path: Union[str, Path]) -> None:
+        """The reference .pt format ({"embeddings": [N, D] f32, "image_paths", "texts"},
+        finder_service.py:93-103), written to a temporary file and renamed into place."""
         path = Path(path)
         path.parent.mkdir(parents=True, exist_ok=True)
-        torch.save({"embeddings": self.embeddings, "image_paths": list(self.image_paths),
-                    "texts": list(self.texts)}, path)
+        tmp = path.with_name(path.name + ".tmp")
+        torch.save({"embeddings": self.embeddings.clone(), "image_paths": list(self.image_paths),
+                    "texts": list(self.texts)}, tmp)
+        tmp.replace(path)

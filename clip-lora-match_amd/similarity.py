@@ -3,9 +3,11 @@
   cosine_similarity  similarity.py:10-33  normalise both sides, (1,d) @ (N,d)^T -> (N,)
   top_k_similar      similarity.py:36-58  topk(min(k, N)) -> (values (k,), indices (k,))
 
-Scores come from the fp16-operand MFMA GEMM with fp32 accumulation and fp32
-norms of the source rows (within 1e-3 of the fp32 CPU reference; typically
-~1e-5); top-k ties are ordered (score desc, index asc).
+Scores are exact: the fp64 cosine of the caller's fp32 vectors, rounded once to
+fp32 (the reference's fp32 matmul of fp32-normalised rows differs from it only by
+its own summation rounding, ~1e-7). top_k_similar bounds its candidates with the
+fp16 MFMA pass and re-scores them exactly (clm_index_search); ties are ordered
+(score desc, index asc).
 """
 from __future__ import annotations
 
@@ -14,7 +16,7 @@ from typing import Tuple
 import torch
 
 from . import _capi as C
-from .search import CosineIndex, _pad_dim
+from .search import CosineIndex
 
 
 def cosine_similarity(query: torch.Tensor, candidates: torch.Tensor) -> torch.Tensor:
@@ -27,13 +29,11 @@ def cosine_similarity(query: torch.Tensor, candidates: torch.Tensor) -> torch.Te
         raise ValueError(f"shape mismatch: query {tuple(q.shape)} vs candidates {tuple(c.shape)}")
     out_dev = c.device
     dev = torch.device("cuda", torch.cuda.current_device())
-    d = q.shape[-1]
-    dp = (d + 63) // 64 * 64
-    qg = _pad_dim(q.float().to(dev), dp).contiguous()
-    cg = _pad_dim(c.float().to(dev), dp).contiguous()
+    qg = q.float().to(dev).contiguous()
+    cg = c.float().to(dev).contiguous()
     out = torch.empty((qg.shape[0], cg.shape[0]), dtype=torch.float32, device=dev)
-    C.check(C.lib().clm_cosine_scores(dev.index, C.ptr(qg), qg.shape[0], C.ptr(cg), cg.shape[0], dp, C.ptr(out),
-                                      C.stream_of(dev)), "clm_cosine_scores")
+    C.check(C.lib().clm_cosine_scores(dev.index, C.ptr(qg), qg.shape[0], C.ptr(cg), cg.shape[0], q.shape[-1],
+                                      C.ptr(out), C.stream_of(dev)), "clm_cosine_scores")
     return out.squeeze(0).to(out_dev)
 
 
@@ -51,7 +51,8 @@ def top_k_similar(query: torch.Tensor, candidates: torch.Tensor, k: int = 5) -> 
         return torch.empty(0), torch.empty(0, dtype=torch.int64)
     idx = CosineIndex(c.shape[1], capacity=c.shape[0])
     try:
-        # the reference normalises the fp32 candidates first (similarity.py:30); store those rows
+        # the reference normalises the fp32 candidates first (similarity.py:30): store those rows
+        # (the exact re-score reads them as given)
         cn = c.float()
         cn = cn / cn.norm(p=2, dim=-1, keepdim=True)
         idx.append(cn)

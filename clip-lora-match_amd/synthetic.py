@@ -39,3 +39,27 @@ def gaussian_rows(n: int, dim: int, seed: int, fp16: bool = True) -> np.ndarray:
     if fp16:
         x = x.astype(np.float16)
     return x
+
+
+def clustered_rows(n_centers: int, per: int, dim: int, noise: float, seed: int, noise_seed=None) -> np.ndarray:
+    """Unit rows in tight clusters (center + Gaussian noise of norm ~`noise`), rows of one
+    cluster contiguous. Top-k scores of a query near a center differ by ~1e-5..1e-4, below
+    the fp16 operand rounding: only an exact re-score orders them like fp32 arithmetic.
+    noise_seed: draw the noise from a separate stream (same centers, fresh noise)."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    c = rng.standard_normal((n_centers, dim)).astype(np.float32)
+    c /= np.linalg.norm(c, axis=-1, keepdims=True)
+    if noise_seed is not None:
+        rng = np.random.Generator(np.random.PCG64(noise_seed))
+    x = np.repeat(c, per, axis=0) + rng.standard_normal((n_centers * per, dim)).astype(np.float32) * \
+        np.float32(noise / np.sqrt(dim))
+    return (x / np.linalg.norm(x, axis=-1, keepdims=True)).astype(np.float32)
+
+
+def fp32_search_inputs():
+    """The fp32 search fixture inputs (tests/golden/search_fp32.npz holds the reference's outputs
+    on them): Gaussian rows [4096, 512] / queries [64, 512], and 64 tight clusters of 64 rows with
+    one query near each center -- all fp32, not fp16-representable."""
+    dim = 512
+    return (gaussian_rows(4096, dim, seed=27, fp16=False), gaussian_rows(64, dim, seed=28, fp16=False),
+            clustered_rows(64, 64, dim, 0.05, seed=29), clustered_rows(64, 1, dim, 0.05, seed=29, noise_seed=30))

@@ -99,8 +99,12 @@ int clm_ctx_destroy(clm_ctx* ctx);
 int clm_load_tensor(clm_ctx* ctx, const char* name, const void* host_ptr, int dtype,
                     const int64_t* shape, int ndim);
 int clm_finalize(clm_ctx* ctx);
-/* drop all LoRA tensors and re-finalize as the base model */
+/* re-finalize with LoRA on (enabled != 0) or off (the base model); tensors are kept */
 int clm_set_lora_enabled(clm_ctx* ctx, int enabled);
+/* attach (or replace) the LoRA configuration of a context in place -- PEFT get_peft_model on
+ * the loaded model (models/lora_adapter.py:46-56): r (0 = none), alpha, CLM_LORA_* targets.
+ * Load the adapter tensors (base_model.model.<path>.lora_{A,B}.weight) next, then clm_finalize. */
+int clm_set_lora(clm_ctx* ctx, int r, float alpha, uint32_t targets);
 
 /* n images -> out [n, proj_dim] (CLM_F32 or CLM_F16); normalize != 0 => unit rows */
 int clm_encode_image(clm_ctx* ctx, const void* pixels, int pix_layout, int n, void* out,
@@ -121,11 +125,14 @@ int clm_encode_pair(clm_ctx* ctx, const void* pixels, int pix_layout, int n_img,
                     int n_txt, int L, void* out_img, void* out_txt, int out_dtype, int normalize,
                     int flags, void* stream);
 
-/* GPU-resident index of fp16 rows + fp32 inverse norms (score = q . row / ||row||) */
+/* GPU-resident cosine index (dim % 64 == 0, <= 1024). Scores are the EXACT cosine of the
+ * caller's query and rows (fp64 arithmetic, rounded once to fp32): an fp16 MFMA pass bounds the
+ * candidates, which are then re-scored against the rows as given. */
 int clm_index_create(int hip_device, int64_t capacity, int dim, clm_index** out);
 int clm_index_destroy(clm_index* idx);
-/* rows [n, dim] CLM_F32|CLM_F16, host or device; stored fp16, inv-norm of the
- * fp16-rounded row in fp32 */
+/* rows [n, dim] CLM_F32|CLM_F16, host or device. Kept: fp16 MFMA operands (f32 rows normalised
+ * then rounded; f16 rows as given) + fp32 inverse norms, and -- once any f32 rows arrive -- an
+ * fp32 copy of the rows as given (f16 rows upcast into it), read by the exact re-score. */
 int clm_index_append(clm_index* idx, const void* rows, int dtype, int64_t n, void* stream);
 int64_t clm_index_size(const clm_index* idx);
 int clm_index_reset(clm_index* idx);
@@ -134,16 +141,21 @@ int clm_index_set_offset(clm_index* idx, int64_t global_offset);
 /* copy rows [start, start+n) back as fp32 (host or device dst) */
 int clm_index_read(clm_index* idx, int64_t start, int64_t n, float* dst, void* stream);
 /* q [nq, dim] CLM_F32|CLM_F16 (normalised in-kernel); k in [1, 1024];
- * out_scores [nq, k] f32, out_idx [nq, k] i64; order: score desc, index asc;
- * slots past the index size are filled with (-inf, -1). */
+ * out_scores [nq, k] f32 = exact cosines, out_idx [nq, k] i64 (+ global offset);
+ * order: score desc, index asc (CPU torch.topk, search.py:98-99, leaves ties unordered);
+ * slots past the index size are filled with (-inf, -1). Replaces the reference's fp32
+ * sims = q_hat @ E_hat^T + topk (search.py:93-99) on the same rows. */
 int clm_index_search(clm_index* idx, const void* q, int q_dtype, int64_t nq, int k,
                      float* out_scores, int64_t* out_idx, void* stream);
 
-/* search-path counters since creation: queries served by the single-pass filtered path,
- * by the exact chunked path, and filtered queries redone exactly after a candidate overflow */
+/* search-path counters since creation: queries served by the sampled single-pass bounded
+ * search (`filtered`), by the exact scan or the fp16-scan-bounded search (`exact`), and
+ * bounded queries redone by the exact scan after a candidate-list overflow */
 int clm_index_stats(const clm_index* idx, int64_t* filtered, int64_t* exact, int64_t* overflow);
+/* out[0..n): sampled bounded, fp16-scan bounded, full exact scan, overflow re-runs */
+int clm_index_stats2(const clm_index* idx, int64_t* out, int n);
 
-/* full cosine matrix: out [nq, n] f32 = normalise(q) . normalise(c)^T */
+/* full cosine matrix, exact: out [nq, n] f32 = fp32(cos64(q_i, c_j)), any dim */
 int clm_cosine_scores(int hip_device, const float* q, int64_t nq, const float* c, int64_t n,
                       int dim, float* out, void* stream);
 

@@ -63,3 +63,18 @@ def encode(model, cfg, pv, ids):
                                      attention_mask=attention_mask(cfg, ids)).pooler_output
         ft = ft / ft.norm(dim=-1, keepdim=True)
     return fi.numpy().astype(np.float32), ft.numpy().astype(np.float32)
+
+
+def encode_images(model, pv):
+    """encode_image semantics only (clip_model.py:115-116), batched: unit rows"""
+    with torch.no_grad():
+        fi = model.get_image_features(pixel_values=pv).pooler_output
+        return fi / fi.norm(dim=-1, keepdim=True)
+
+
+def encode_texts(model, cfg, ids):
+    """encode_text semantics only (clip_model.py:144-148), batched: unit rows"""
+    with torch.no_grad():
+        ft = model.get_text_features(input_ids=torch.from_numpy(ids).long(),
+                                     attention_mask=attention_mask(cfg, ids)).pooler_output
+        return ft / ft.norm(dim=-1, keepdim=True)

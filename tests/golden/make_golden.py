@@ -111,8 +111,30 @@ def search_golden():
     print("custom_index_top3.npz", idx.tolist())
 
 
+def search_fp32_golden():
+    """fp32 (not fp16-representable) rows and queries through the reference's own
+    similarity.top_k_similar / cosine_similarity: Gaussian and tightly clustered sets."""
+    sim = _load_ref_similarity()
+    dim = 512
+    gauss_rows, gauss_q, clus, clus_q = syn.fp32_search_inputs()
+    out = dict(dim=np.array(dim))   # inputs are regenerated from their seeds (fp32_search_inputs)
+    for name, rows, qs in (("gauss", gauss_rows, gauss_q), ("clus", clus, clus_q)):
+        E = torch.from_numpy(rows)
+        for k in (1, 5, 10, 50):
+            vals = np.zeros((qs.shape[0], k), np.float32)
+            idx = np.zeros((qs.shape[0], k), np.int64)
+            for i in range(qs.shape[0]):
+                v, ix = sim.top_k_similar(torch.from_numpy(qs[i]), E, k)
+                vals[i], idx[i] = v.numpy(), ix.numpy()
+            out[f"{name}_vals_k{k}"] = vals
+            out[f"{name}_idx_k{k}"] = idx
+        out[f"{name}_cos_q0"] = sim.cosine_similarity(torch.from_numpy(qs[0]), E).numpy().astype(np.float32)
+    np.savez_compressed(os.path.join(HERE, "search_fp32.npz"), **out)
+    print("search_fp32.npz")
+
+
 if __name__ == "__main__":
-    which = sys.argv[1:] or ["tiny", "b32", "l14", "search"]
+    which = sys.argv[1:] or ["tiny", "b32", "l14", "search", "search_fp32"]
     if "tiny" in which:
         encoder_golden("enc_tiny_lora.npz", "tiny", 4, 4, 16, True)
     if "b32" in which:
@@ -121,3 +143,5 @@ if __name__ == "__main__":
         encoder_golden("enc_l14_lora.npz", "ViT-L/14@336", 2, 2, 77, True)
     if "search" in which:
         search_golden()
+    if "search_fp32" in which:
+        search_fp32_golden()

@@ -1,0 +1,53 @@
+"""Multi-rank GPU paths on one MI355X: world 2 over gloo (RCCL refuses two ranks
+per device; the driver's 8-GPU node runs the RCCL path). The product's own sharded index build
+and row-sharded search with the GPU merge must equal the single-rank results bit for bit, and
+bench.py --gpus 2 must start and report 2 ranks by itself."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+from conftest import REPO
+
+pytestmark = pytest.mark.gpu
+
+
+def _port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def test_sharded_build_and_search_world2(tmp_path):
+    out = tmp_path / "res.json"
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr=127.0.0.1", f"--master-port={_port()}", os.path.join(REPO, "tests", "dist_gpu_worker.py"),
+           str(out), str(tmp_path)]
+    p = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=240)
+    assert p.returncode == 0, p.stderr[-3000:]
+    r = json.loads(out.read_text())
+    assert r["world"] == 2
+    assert r["file_rows_rank0"] == 37 and r["file_rows_rank1"] == 37
+    for key in ("build_img_equal", "build_txt_equal", "file_equal", "search_idx_equal", "search_scores_equal",
+                "merge_roundtrip"):
+        assert r[key], key
+    assert r["planted_top1"] == [5, 150_000, 150_001, 299_999]
+
+
+def test_bench_spawns_its_own_ranks(tmp_path):
+    """bench.py --gpus 2 with no launcher around it starts 2 ranks itself (gloo rehearsal on a
+    1-GPU box) and reports n_gpus 2 from a 2-rank process group."""
+    cmd = [sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2", "--steps", "2", "--warmup", "1",
+           "--batch", "32", "--no-cpu-baseline", "--no-l14", "--no-parity-mode", "--search-rows", "600000",
+           "--search-queries", "256"]
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=str(tmp_path))
+    assert p.returncode == 0, p.stderr[-3000:]
+    line = [ln for ln in p.stdout.splitlines() if ln.startswith("{")][-1]
+    r = json.loads(line)
+    assert r["n_gpus"] == 2 and r["dist"]["world_size"] == 2
+    assert r["search"]["n_gpus"] == 2 and r["search"]["qps"] > 0
+    assert r["value"] > 0

@@ -97,3 +97,23 @@ def test_fuse_query_oracle_is_seeker_service_rule():
     np.testing.assert_allclose(np.sum(f * t, -1), np.sum(f * i, -1), atol=1e-6)
     with pytest.raises(ValueError):
         S.fuse_query(None, None)
+
+
+@pytest.mark.parametrize("name", ["gauss", "clus"])
+@pytest.mark.parametrize("k", [1, 5, 10, 50])
+def test_search_oracle_vs_reference_fp32_golden(name, k):
+    """fp32 (not fp16-representable) rows/queries: the oracle's exact (fp64) ranking equals the
+    reference's fp32 top_k_similar up to 2e-6 near-ties, and its scores match to fp32 rounding.
+    The clustered set has top-k scores 1e-5..1e-4 apart (below fp16 operand rounding)."""
+    g = golden("search_fp32.npz")
+    gr, gq, cr, cq = syn.fp32_search_inputs()
+    rows, qs = (gr, gq) if name == "gauss" else (cr, cq)
+    exact = S.cosine_scores(qs, rows)
+    vals, idx = S.topk(exact, k)
+    for q in range(qs.shape[0]):
+        assert S.same_topk_up_to_ties(idx[q], g[f"{name}_idx_k{k}"][q], exact[q], 2e-6)
+    assert np.max(np.abs(vals - g[f"{name}_vals_k{k}"])) < 1e-6
+    assert np.max(np.abs(exact[0] - g[f"{name}_cos_q0"])) < 1e-6
+    if name == "clus" and k == 10:   # the fixture is non-trivial: neighbours closer than fp16 resolution
+        gaps = -np.diff(vals, axis=1)
+        assert np.median(gaps) < 1e-4
