@@ -19,7 +19,7 @@ from clip_lora_match_amd import synthetic as syn  # noqa: E402
 from clip_lora_match_amd import weights as W  # noqa: E402
 from clip_lora_match_amd.distributed import ShardedIndex, merge_topk_gpu  # noqa: E402
 from clip_lora_match_amd.engine import ClipLoraModel  # noqa: E402
-from clip_lora_match_amd.index_build import encode_items, rebuild_index  # noqa: E402
+from clip_lora_match_amd.index_build import _renormalize, encode_items, rebuild_index  # noqa: E402
 from clip_lora_match_amd.processor import ClipProcessor  # noqa: E402
 from clip_lora_match_amd.search import CosineIndex  # noqa: E402
 
@@ -43,7 +43,11 @@ def main(out_path, tmpdir):
                           batch_size=8)
     # every rank may read the file right after rebuild_index returns
     obj = torch.load(os.path.join(tmpdir, "idx.pt"), map_location="cpu", weights_only=True)
-    res[f"file_rows_rank{rank}"] = int(obj["embeddings"].shape[0])
+    fr = torch.tensor([int(obj["embeddings"].shape[0])])
+    lo, hi = fr.clone(), fr.clone()
+    dist.all_reduce(lo, op=dist.ReduceOp.MIN)
+    dist.all_reduce(hi, op=dist.ReduceOp.MAX)
+    res["file_rows_min_max"] = [int(lo), int(hi)]
     # 2. row-sharded search: 300k fp32 rows, each rank holds its shard_range
     n, dim, nq, k = 300_000, 512, 24, 10
     rows = syn.gaussian_rows(n, dim, 41, fp16=False)
@@ -55,9 +59,11 @@ def main(out_path, tmpdir):
     dist.barrier()
     if rank == 0:
         # single-rank references
-        ref_img = torch.cat([model.encode_pixels(torch.from_numpy(np.stack(imgs[a:a + 8])).cuda())
+        # (encode_items re-normalises each row once more, as rebuild_index.py:72 does)
+        ref_img = torch.cat([_renormalize(model.encode_pixels(torch.from_numpy(np.stack(imgs[a:a + 8])).cuda()))
                              for a in range(0, 37, 8)]).cpu()
-        ref_txt = torch.cat([model.encode_ids(proc.token_ids(caps[a:a + 8]).cuda()) for a in range(0, 37, 8)]).cpu()
+        ref_txt = torch.cat([_renormalize(model.encode_ids(proc.token_ids(caps[a:a + 8]).cuda()))
+                             for a in range(0, 37, 8)]).cpu()
         res["build_img_equal"] = bool(torch.equal(e_img.cpu(), ref_img))
         res["build_txt_equal"] = bool(torch.equal(e_txt, ref_txt))
         res["file_equal"] = bool(torch.equal(obj["embeddings"], ref_txt))

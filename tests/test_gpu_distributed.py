@@ -31,7 +31,7 @@ def test_sharded_build_and_search_world2(tmp_path):
     assert p.returncode == 0, p.stderr[-3000:]
     r = json.loads(out.read_text())
     assert r["world"] == 2
-    assert r["file_rows_rank0"] == 37 and r["file_rows_rank1"] == 37
+    assert r["file_rows_min_max"] == [37, 37]     # both ranks read the complete file
     for key in ("build_img_equal", "build_txt_equal", "file_equal", "search_idx_equal", "search_scores_equal",
                 "merge_roundtrip"):
         assert r[key], key

@@ -125,7 +125,7 @@ def test_all_paths_agree_bit_for_bit(monkeypatch):
 def test_sample_cache_invalidated_by_reset(monkeypatch):
     """clm_index_reset / append drop the threshold sample: refilling the same row count with
     different rows must not reuse the old rows' sample (a stale theta could drop true top-k)."""
-    n, dim, nq = 1_000_000, 256, 16
+    n, dim, nq = 1_000_000, 256, 32   # nq * n > 2^24: the bounded (sampled) search serves
     idx = CosineIndex(dim, capacity=n)
     for seed in (1, 2):
         g = torch.Generator(device="cuda").manual_seed(seed)
@@ -277,9 +277,10 @@ def test_filtered_path_equals_exact_path(k, monkeypatch):
     assert idx.stats()["exact"] == 2 * nq
 
 
-def test_filtered_path_overflow_falls_back():
+def test_filtered_path_overflow_falls_back(monkeypatch):
     """300k identical rows make every one of them a candidate (> capacity): those queries
     are redone exactly and return the k smallest indices of the tie group."""
+    monkeypatch.setenv("CLM_SEARCH_BOUNDED", "1")   # 2 queries x 1M rows: small enough for the full scan
     n, dim = 1_000_000, 128
     g = torch.Generator(device="cuda").manual_seed(3)
     rows = torch.randn((n, dim), generator=g, device="cuda")
