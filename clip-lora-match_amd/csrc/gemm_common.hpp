@@ -297,6 +297,8 @@ constexpr int epi_min_stores() {
 
 }  // namespace gemm_detail
 
-// G2 kernels (k_gemm2.hip): configs 11-13
+// G2 kernels (k_gemm2.hip): configs 11-22
 hipError_t gemm2_launch(bool bf16, int epi, int id, const GemmArgs& g, hipStream_t s);
+// G3 kernel (k_gemm3.hip): config 23, 256 x 256 eight-phase ping-pong
+hipError_t gemm3_launch(bool bf16, int epi, const GemmArgs& g, hipStream_t s);
 }  // namespace clm

@@ -223,11 +223,12 @@ hipError_t launch_id(int id, const GemmArgs& g, hipStream_t s) {
     case 10: return launch_cfg<BF, EPI, 128, 256, 2, 4, 2>(g, s);
     case 11: case 12: case 13: case 14: case 15: case 16: case 17: case 18: case 19: case 20: case 21: case 22:
       return gemm2_launch(BF, EPI, id, g, s);
+    case 23: return gemm3_launch(BF, EPI, g, s);
     default: return hipErrorInvalidValue;
   }
 }
 
-constexpr int NCFG = 23;
+constexpr int NCFG = 24;
 
 // Tile choice: a cost model per kernel family, time(cfg) ~ rounds(cfg) x round_cost(cfg),
 // rounds = ceil(tiles / resident workgroups), round_cost = BM*BN*(workgroups per CU) /

@@ -77,13 +77,28 @@ def test_b32_unmerged_matches_merged():
     _check(gi, gt, g["emb_img"], g["emb_txt"], "float16")
 
 
-def test_l14_lora_golden():
+# configs[3] (ViT-L/14@336 + LoRA r=16 on attention and MLP) at its configured bf16 precision:
+# twice the depth of B/32 (24 vision layers; bf16 operand rounding errors accumulate roughly with
+# the square root of the number of rounded GEMM inputs along the path) and a rank-16 adapter on
+# every Linear, so the B/32 bf16 bars scale by ~sqrt(2): scores 6e-3, 1 - cos 2e-4 (measured on
+# MI355X: see DESIGN.md §Numerics). fp16 keeps the north_star 1e-3 bar.
+TOL_L14 = {"float16": dict(score=1e-3, cos=1e-5), "bfloat16": dict(score=6e-3, cos=2e-4)}
+
+
+@pytest.mark.parametrize("dtype", ["float16", "bfloat16"])
+def test_l14_lora_golden(dtype):
     g = golden("enc_l14_lora.npz")
-    m, cfg, _, _ = _model("ViT-L/14@336", "float16", max_batch=8)
+    m, cfg, _, _ = _model("ViT-L/14@336", dtype, max_batch=8)
     imgs = syn.images_u8(int(g["n_img"]), cfg.image_size, int(g["img_seed"]))
     gi = m.encode_pixels(torch.from_numpy(imgs).cuda()).cpu().numpy()
     gt = m.encode_ids(torch.from_numpy(g["ids"]).cuda()).cpu().numpy()
-    _check(gi, gt, g["emb_img"], g["emb_txt"], "float16")
+    ri, rt = g["emb_img"], g["emb_txt"]
+    cos = [float(np.max(1 - np.sum(a * b, -1) / (np.linalg.norm(a, axis=-1) * np.linalg.norm(b, axis=-1))))
+           for a, b in ((gi, ri), (gt, rt))]
+    err = max(float(np.max(np.abs(x @ y.T - xr @ yr.T))) for x, y, xr, yr in
+              ((gi, gi, ri, ri), (gi, gt, ri, rt), (gt, gt, rt, rt)))
+    print(f"L/14 {dtype}: max score error {err:.3e}, max 1 - cos {max(cos):.3e}")
+    assert max(cos) <= TOL_L14[dtype]["cos"] and err <= TOL_L14[dtype]["score"], (err, cos)
 
 
 def test_pixel_layouts_and_host_pointers():

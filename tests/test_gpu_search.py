@@ -392,3 +392,66 @@ def test_build_query_embedding_and_search_items(tmp_path):
     assert res[0].index == 17 and res[0].image_path == "p17" and abs(res[0].score - 1.0) < 1e-3
     with pytest.raises(FileNotFoundError):
         search_items(index, m, proc, dev, query_text=row, query_image_path="missing.png", root_dir=tmp_path)
+
+
+def test_full_size_config4_index():
+    """configs[4] at its full size: 10 M x 512 fp16 rows in HBM, 512 queries (a planted copy of
+    a row for the first 64). Planted rows come back at rank 0 with score 1; the sampled bounded
+    search equals the full exact scan bit for bit on a query subset; and a host check of 4
+    queries (fp32 scan of every row in 1 M-row chunks, then an fp64 re-score of each chunk's
+    top 64) gives the same top-5 up to 2e-6 near-ties."""
+    n, dim, nq, k = 10_000_000, 512, 512, 5
+    idx = CosineIndex(dim, capacity=n)
+    g = torch.Generator(device="cuda").manual_seed(77)
+    chunk = 1 << 20
+    host = []
+    for r0 in range(0, n, chunk):
+        x = torch.randn((min(chunk, n - r0), dim), generator=g, device="cuda")
+        xh = (x / x.norm(dim=-1, keepdim=True)).half()
+        idx.append(xh)
+        host.append(xh.cpu())
+        del x, xh
+    rows = torch.cat(host)
+    del host
+    plant = torch.randint(0, n, (64,), generator=g)
+    q = torch.randn((nq, dim), generator=g).half()
+    q[:64] = rows[plant]
+    s, i = idx.search(q.cuda(), k)
+    assert idx.stats()["filtered"] == nq
+    assert torch.equal(i[:64, 0].cpu(), plant) and torch.all(s[:64, 0] == 1.0)
+    assert torch.all(s[:, 1:] <= s[:, :-1])
+    import os
+    os.environ["CLM_SEARCH_FULL"] = "1"
+    try:
+        s2, i2 = idx.search(q[64:96].cuda(), k)
+    finally:
+        del os.environ["CLM_SEARCH_FULL"]
+    assert torch.equal(i2, i[64:96]) and torch.equal(s2, s[64:96])
+    qs = q[100:104].float().numpy().astype(np.float64)
+    qs /= np.linalg.norm(qs, axis=-1, keepdims=True)
+    cand = []
+    for r0 in range(0, n, chunk):
+        blk = rows[r0:r0 + chunk].float()
+        sc = (torch.from_numpy(qs).float() @ blk.T)
+        cand.append(torch.topk(sc, 64, dim=1).indices + r0)
+    cand = torch.cat(cand, 1).numpy()
+    for j in range(4):
+        c = np.unique(cand[j])
+        rr = rows[c].double().numpy()
+        ex = (rr @ qs[j]) / np.linalg.norm(rr, axis=-1)
+        order = np.lexsort((c, -ex))[:k]
+        exd = dict(zip(c.tolist(), ex.tolist()))
+        got = i[100 + j].cpu().numpy()
+        assert S.same_topk_up_to_ties(got, c[order], _sparse_scores(exd, n), 2e-6), (j, got, c[order])
+        assert np.max(np.abs(s[100 + j].cpu().numpy() - ex[order])) < 1e-6
+
+
+class _sparse_scores:
+    """exact scores by global row index for the rows a check looked at (same_topk_up_to_ties
+    indexes its `exact_scores` argument by row)"""
+
+    def __init__(self, d, n):
+        self.d = d
+
+    def __getitem__(self, idx):
+        return np.array([self.d.get(int(t), -9.0) for t in np.atleast_1d(idx)])

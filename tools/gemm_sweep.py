@@ -32,7 +32,9 @@ def main():
         out = torch.zeros((M, N), device=dev, dtype=torch.float32 if epi == C.CLM_EPI_RESID else torch.bfloat16)
         bias = torch.zeros(N, device=dev)
         bufs[name] = (A, W, out, bias)
-    cfgs = list(range(ncfg)) + [-1, "hipblaslt"]   # hipblaslt: torch.matmul, bf16 out, no epilogue
+    only = os.environ.get("SWEEP_CFGS")
+    cfgs = ([int(c) if c.lstrip("-").isdigit() else c for c in only.split(",")] if only
+            else list(range(ncfg)) + [-1, "hipblaslt"])   # hipblaslt: torch.matmul, bf16 out, no epilogue
     obf = {n: torch.empty((b[0].shape[0], b[1].shape[0]), device=dev, dtype=torch.bfloat16) for n, b in bufs.items()}
     for rnd in range(3):
         for name, (M, N, K, epi) in SHAPES.items():
