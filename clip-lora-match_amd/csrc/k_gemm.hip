@@ -209,6 +209,11 @@ hipError_t launch_cfg(const GemmArgs& g, hipStream_t s) {
 // tile configurations (index = GemmArgs-independent id, also the `config` of clm_gemm)
 template <bool BF, int EPI>
 hipError_t launch_id(int id, const GemmArgs& g, hipStream_t s) {
+  if constexpr (epi_ln(EPI)) {   // LayerNorm-folded epilogues: the TN <= 4 tiles of G2 / G3 only
+    if (id == 23) return gemm3_launch(BF, EPI, g, s);
+    if (id >= 16 && id <= 18) return gemm2_launch(BF, EPI, id, g, s);
+    return hipErrorInvalidValue;
+  } else {
   switch (id) {
     case 0: return launch_cfg<BF, EPI, 128, 128, 2, 2, 2>(g, s);
     case 1: return launch_cfg<BF, EPI, 128, 128, 2, 2, 3>(g, s);
@@ -225,6 +230,7 @@ hipError_t launch_id(int id, const GemmArgs& g, hipStream_t s) {
       return gemm2_launch(BF, EPI, id, g, s);
     case 23: return gemm3_launch(BF, EPI, g, s);
     default: return hipErrorInvalidValue;
+  }
   }
 }
 
@@ -270,6 +276,12 @@ int pick_config(int epi, int M, int N) {
     const char* e = getenv("CLM_GEMM_CFG");
     forced = e ? atoi(e) : -1;
   }
+  if (epi_ln(epi)) {   // LayerNorm-folded epilogues (TN <= 4 tiles): qkv -> G3, fc1 -> G2 16 / 17 / 18
+    if (forced == 23 || (forced >= 16 && forced <= 18)) return forced;
+    if (epi == EPI_STORE_LN) return 23;
+    constexpr CfgModel MODELS_LN[] = {{16, 256, 128, 1, 2.349}, {17, 192, 256, 1, 2.521}, {18, 128, 256, 1, 2.340}};
+    return pick_from(MODELS_LN, M, N);
+  }
   if (forced >= 0 && forced < NCFG) return forced;
   static int g2_epis = -1;   // epilogues served by G2 (bit per Epi); $CLM_G2_EPIS overrides
   if (g2_epis < 0) {
@@ -305,6 +317,8 @@ hipError_t dispatch(int epi, int id, const GemmArgs& g, hipStream_t s) {
     case EPI_PATCH: return launch_id<BF, EPI_PATCH>(id, g, s);
     case EPI_SCORE: return launch_id<BF, EPI_SCORE>(id, g, s);
     case EPI_FILTER: return launch_id<BF, EPI_FILTER>(id, g, s);
+    case EPI_STORE_LN: return launch_id<BF, EPI_STORE_LN>(id, g, s);
+    case EPI_GELU_LN: return launch_id<BF, EPI_GELU_LN>(id, g, s);
     default: return hipErrorInvalidValue;
   }
 }
@@ -320,5 +334,6 @@ hipError_t gemm_cfg(bool bf16, int epi, int config, const GemmArgs& g, hipStream
 }
 
 hipError_t gemm(bool bf16, int epi, const GemmArgs& g, hipStream_t s) { return gemm_cfg(bf16, epi, -1, g, s); }
+
 
 }  // namespace clm

@@ -281,6 +281,14 @@ hipError_t launch_cfg2(const GemmArgs& g, hipStream_t s) {
 
 template <bool BF, int EPI>
 hipError_t by_id(int id, const GemmArgs& g, hipStream_t s) {
+  if constexpr (epi_ln(EPI)) {   // LayerNorm-folded epilogues: TN <= 4 tiles only
+    switch (id) {
+      case 16: return launch_cfg2<BF, EPI, 256, 128, 4, 2>(g, s);
+      case 17: return launch_cfg2<BF, EPI, 192, 256, 2, 4>(g, s);
+      case 18: return launch_cfg2<BF, EPI, 128, 256, 2, 4>(g, s);
+      default: return hipErrorInvalidValue;
+    }
+  } else {
   switch (id) {
     case 11: return launch_cfg2<BF, EPI, 256, 256, 2, 2>(g, s);
     case 12: return launch_cfg2<BF, EPI, 256, 128, 2, 2>(g, s);
@@ -300,6 +308,7 @@ hipError_t by_id(int id, const GemmArgs& g, hipStream_t s) {
     case 22: return launch_cfg2<BF, EPI, 128, 256, 2, 4, false, 3>(g, s);
     default: return hipErrorInvalidValue;
   }
+  }
 }
 template <bool BF>
 hipError_t by_epi(int epi, int id, const GemmArgs& g, hipStream_t s) {
@@ -310,6 +319,8 @@ hipError_t by_epi(int epi, int id, const GemmArgs& g, hipStream_t s) {
     case EPI_PATCH: return by_id<BF, EPI_PATCH>(id, g, s);
     case EPI_SCORE: return by_id<BF, EPI_SCORE>(id, g, s);
     case EPI_FILTER: return by_id<BF, EPI_FILTER>(id, g, s);
+    case EPI_STORE_LN: return by_id<BF, EPI_STORE_LN>(id, g, s);
+    case EPI_GELU_LN: return by_id<BF, EPI_GELU_LN>(id, g, s);
     default: return hipErrorInvalidValue;
   }
 }

@@ -218,6 +218,8 @@ hipError_t by_epi3(int epi, const GemmArgs& g, hipStream_t s) {
     case EPI_PATCH: return launch3<BF, EPI_PATCH>(g, s);
     case EPI_SCORE: return launch3<BF, EPI_SCORE>(g, s);
     case EPI_FILTER: return launch3<BF, EPI_FILTER>(g, s);
+    case EPI_STORE_LN: return launch3<BF, EPI_STORE_LN>(g, s);
+    case EPI_GELU_LN: return launch3<BF, EPI_GELU_LN>(g, s);
     default: return hipErrorInvalidValue;
   }
 }
