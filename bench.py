@@ -293,7 +293,7 @@ def search_leg(rows: int, queries: int, k: int, device, world: int = 1, rank: in
             s, i = merge_topk_gpu(s_all, i_all, world, k)
         return s, i
 
-    run(q[:64])
+    run(q)   # untimed pass of the same shape: the index's search workspace is sized here
     torch.cuda.synchronize()
     if world > 1:
         torch.distributed.barrier()

@@ -10,8 +10,8 @@ import os, sys, json, torch
 sys.path.insert(0, os.getcwd())
 import bench
 dev = torch.device("cuda", 0)
-r = bench.search_leg(int(os.environ.get("ROWS", "10000000")), 10000, 5, dev)
-r2 = bench.search_leg(int(os.environ.get("ROWS", "10000000")), 10000, 5, dev)
+r = bench.search_leg(int(os.environ.get("ROWS", "10000000")), 10000, 5, dev)[0]
+r2 = bench.search_leg(int(os.environ.get("ROWS", "10000000")), 10000, 5, dev)[0]
 print(json.dumps({"s1": r["seconds"], "s2": r2["seconds"], "qps": max(r["qps"], r2["qps"])}))
 '''
 for spec in sys.argv[1:]:
