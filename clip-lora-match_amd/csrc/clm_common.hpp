@@ -36,12 +36,24 @@ __device__ __forceinline__ u16 f32_to_f16(float f) { return __builtin_bit_cast(u
 template <bool BF> __device__ __forceinline__ float to_f32(u16 v) { return BF ? bf16_to_f32(v) : f16_to_f32(v); }
 template <bool BF> __device__ __forceinline__ u16 from_f32(float f) { return BF ? f32_to_bf16(f) : f32_to_f16(f); }
 
-// pack two floats into one dword of two 16-bit values (lo first)
-// (two scalar RNE casts + shift/or: hipcc folds the bf16 pair into v_cvt_pk_bf16_f32 by
-// itself; a __builtin_convertvector pair form measured 10-20 % slower GEMM epilogues and a
-// 2x slower patchify in the encode pipeline)
+// pack two floats into one dword of two 16-bit values (lo first), RNE.
+// The two-element vector conversion is ONE v_cvt_pk_bf16_f32 / v_cvt_pk_f16_f32; the form
+// with two scalar casts + shift / or compiles (ROCm 7.2) to two half-used v_cvt_pk_bf16_f32,
+// a shift and an SDWA or -- 4 VALU per pair (3 for fp16) in every epilogue and in attention's
+// P packing. Same instruction, same rounding: results are bit-identical.
+// (-DCLM_PACK_SCALAR builds the old form for A/B runs.)
+typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+typedef _Float16 f16x2_t __attribute__((ext_vector_type(2)));
+typedef float f32x2_t __attribute__((ext_vector_type(2)));
 template <bool BF> __device__ __forceinline__ uint32_t pack2(float a, float b) {
+#ifdef CLM_PACK_SCALAR
   return (uint32_t)from_f32<BF>(a) | ((uint32_t)from_f32<BF>(b) << 16);
+#else
+  if constexpr (BF)
+    return __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2_t{a, b}, bf16x2_t));
+  else
+    return __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2_t{a, b}, f16x2_t));
+#endif
 }
 
 // one 16x16x32 MFMA on 8-element fragments held as raw 16-byte vectors

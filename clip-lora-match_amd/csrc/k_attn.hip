@@ -198,6 +198,193 @@ __global__ __launch_bounds__(256, CAUSAL ? 2 : 3) void attn_kernel(const u16* qk
   }
 }
 
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+template <bool BF>
+__device__ __forceinline__ f32x16 mfma32(const u32x4& a, const u32x4& b, f32x16 c) {
+  if constexpr (BF)
+    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), c,
+                                                   0, 0, 0);
+  else
+    return __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8, a), __builtin_bit_cast(f16x8, b), c, 0,
+                                                  0, 0);
+}
+
+// max / sum of v over lanes l and l ^ 32 (v_permlane32_swap: a VALU exchange, no LDS round trip;
+// with both operands v the two results are v's lower and upper halves, each broadcast)
+__device__ __forceinline__ float pair32_max(float v) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+__device__ __forceinline__ float pair32_sum(float v) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+
+// V^T operand (32 dims x 16 keys) of a 32x32x16 PV MFMA, from the row-major swizzled V tile.
+// Lane l (hi = l >> 5) holds dim dim0 + (l & 31) and logical k = 8 hi + t, t = 0..7, standing for
+// key k16 + 4 hi + t (t < 4) or k16 + 8 + 4 hi + (t - 4): the order in which the 32x32 S^T
+// accumulator leaves P in the lane (C row 8 (r >> 2) + 4 hi + (r & 3)), so P feeds the MFMA
+// straight from registers. Two ds_read_b64_tr_b16, each 16-lane group reading 4 key rows x 16 dims.
+__device__ __forceinline__ u32x4 v_frag32(const uint8_t* tile, int k16, int dim0, int lane) {
+  const int gg = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
+  const int hi = gg >> 1, dh = gg & 1;
+  const int chunk = (dim0 >> 3) + 2 * dh + (p >> 1);
+  const int ka = k16 + 4 * hi + q, kb = ka + 8;
+  const uint8_t* pa = tile + ka * 128 + ((chunk ^ ((ka >> 1) & 7)) << 4) + (p & 1) * 8;
+  const uint8_t* pb = tile + kb * 128 + ((chunk ^ ((kb >> 1) & 7)) << 4) + (p & 1) * 8;
+  const s16x4 ra = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)pa);
+  const s16x4 rb = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)pb);
+  const u32x2 a = __builtin_bit_cast(u32x2, ra), b = __builtin_bit_cast(u32x2, rb);
+  return u32x4{a.x, a.y, b.x, b.y};
+}
+
+// T > 128, non-causal (ViT-L/14@336: T = 577) on 32x32x16 MFMAs. One workgroup = 4 waves x 32
+// queries of one (batch, head); the workgroups of a (batch, head) are consecutive on one XCD
+// (xcd_remap), so its K / V rows are fetched into that XCD's L2 once. Per 64-key tile:
+//   S^T = K Q^T as 2 key blocks of 32: lane l holds query (l & 31) and 32 of the tile's keys, the
+//     other 32 in lane l ^ 32 -> row max = in-lane v_max3 chain + one v_permlane32_swap;
+//   online softmax in the log2 domain; O and the running sum are rescaled only when some row's
+//     max grew (wave vote; exp2(0) = 1 otherwise, so skipping is exact); row sums stay per lane
+//     until the end;
+//   O^T += V^T P^T: P packed from the accumulators is the B operand as it lies (v_frag32 reads V
+//     in the matching key order).
+// K / V tiles double-buffered in LDS, the next tile loaded into registers during this one's
+// MFMAs (one barrier per tile). Waves whose 32 queries all lie past T only stage tiles.
+template <bool BF>
+__global__ __launch_bounds__(256, 2) void attn_long_kernel(const u16* qkv, int64_t ldq, u16* out, int64_t ldo,
+                                                           int T, int d, int H, int nqb) {
+  constexpr float L2E = 1.4426950408889634f;
+  __shared__ __attribute__((aligned(16))) uint8_t smem[2 * 16384];
+  const int nwg = gridDim.x;
+  const int wg = xcd_remap(blockIdx.x, nwg);
+  const int qb = wg % nqb, bh = wg / nqb, h = bh % H, b = bh / H;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, hi = lane >> 5;
+  const u16* base = qkv + (int64_t)b * T * ldq;
+  const int qw = qb * 128 + wid * 32;   // first query of this wave
+  const bool active = qw < T;
+  const int qi = qw + (lane & 31);
+
+  u32x4 qf[4];   // Q^T operand: query qi, dims 16 s + 8 hi + 0..7
+  {
+    const u16* qp = base + (int64_t)min(qi, T - 1) * ldq + h * 64 + 8 * hi;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) qf[s] = *(const u32x4*)(qp + 16 * s);
+  }
+  f32x16 o[2];   // O^T: query qi, dims db * 32 + 8 (r >> 2) + 4 hi + (r & 3)
+#pragma unroll
+  for (int db = 0; db < 2; ++db)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) o[db][r] = 0.f;
+  float m = -INFINITY, l = 0.f;   // running max (log2 domain, shared by lanes l, l^32); lane-partial sum
+
+  const int nkt = (T + 63) / 64;
+  u32x4 kr[2], vr[2];
+  auto load = [&](int kt) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int ci = tid + 256 * i, key = ci >> 3, c = ci & 7, kg = kt * 64 + key;
+      kr[i] = u32x4{0u, 0u, 0u, 0u};
+      vr[i] = u32x4{0u, 0u, 0u, 0u};
+      if (kg < T) {
+        const u16* rp = base + (int64_t)kg * ldq + h * 64 + c * 8;
+        kr[i] = *(const u32x4*)(rp + d);
+        vr[i] = *(const u32x4*)(rp + 2 * d);
+      }
+    }
+  };
+  auto stage = [&](int buf) {
+    uint8_t* sK = smem + buf * 16384;
+    uint8_t* sV = sK + 8192;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int ci = tid + 256 * i, key = ci >> 3, c = ci & 7;
+      *(u32x4*)(sK + key * 128 + swz(key, c) * 16) = kr[i];
+      *(u32x4*)(sV + key * 128 + swz(key, c) * 16) = vr[i];
+    }
+  };
+  load(0);
+  stage(0);
+  if (nkt > 1) load(1);
+  __syncthreads();
+  for (int kt = 0; kt < nkt; ++kt) {
+    if (active) {
+      const uint8_t* sK = smem + (kt & 1) * 16384;
+      const uint8_t* sV = sK + 8192;
+      const int kleft = T - kt * 64;   // valid keys in this tile (>= 1)
+      f32x16 sc[2];
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) sc[kb][r] = 0.f;
+        const int krow = kb * 32 + (lane & 31);
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          const u32x4 kf = *(const u32x4*)(sK + krow * 128 + swz(krow, 2 * s + hi) * 16);
+          sc[kb] = mfma32<BF>(kf, qf[s], sc[kb]);
+        }
+      }
+      if (kleft < 64) {
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+          for (int r = 0; r < 16; ++r)
+            if (kb * 32 + 8 * (r >> 2) + 4 * hi + (r & 3) >= kleft) sc[kb][r] = -INFINITY;
+      }
+      float tmax = sc[0][0];
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) tmax = fmaxf(tmax, sc[kb][r]);
+      tmax = pair32_max(tmax);
+      const float mnew = fmaxf(m, tmax * L2E);   // finite: every tile holds a valid key
+      if (__any(mnew > m)) {
+        const float alpha = __builtin_amdgcn_exp2f(m - mnew);   // 0 on the first tile, 1 where no growth
+        l *= alpha;
+#pragma unroll
+        for (int db = 0; db < 2; ++db)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) o[db][r] *= alpha;
+        m = mnew;
+      }
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb) {
+        u32x4 pf[2];
+#pragma unroll
+        for (int hf = 0; hf < 2; ++hf) {
+          float p[8];
+#pragma unroll
+          for (int t = 0; t < 8; ++t) {
+            p[t] = __builtin_amdgcn_exp2f(fmaf(sc[kb][8 * hf + t], L2E, -m));
+            l += p[t];
+          }
+          pf[hf] = u32x4{pack2<BF>(p[0], p[1]), pack2<BF>(p[2], p[3]), pack2<BF>(p[4], p[5]), pack2<BF>(p[6], p[7])};
+        }
+#pragma unroll
+        for (int hf = 0; hf < 2; ++hf)
+#pragma unroll
+          for (int db = 0; db < 2; ++db) o[db] = mfma32<BF>(v_frag32(sV, kb * 32 + 16 * hf, db * 32, lane), pf[hf], o[db]);
+      }
+    }
+    if (kt + 1 < nkt) {
+      stage((kt + 1) & 1);
+      if (kt + 2 < nkt) load(kt + 2);
+    }
+    __syncthreads();
+  }
+  if (!active) return;
+  l = pair32_sum(l);
+  if (qi >= T) return;
+  const float inv = 1.0f / l;
+  u16* op = out + ((int64_t)b * T + qi) * ldo + h * 64 + 4 * hi;
+#pragma unroll
+  for (int db = 0; db < 2; ++db)
+#pragma unroll
+    for (int g = 0; g < 4; ++g)
+      *(u32x2*)(op + db * 32 + 8 * g) = u32x2{pack2<BF>(o[db][4 * g] * inv, o[db][4 * g + 1] * inv),
+                                              pack2<BF>(o[db][4 * g + 2] * inv, o[db][4 * g + 3] * inv)};
+}
+
 // T <= 128 (ViT-B/32: vision T = 50, text T = 77 causal): one workgroup per (head, batch),
 // ceil(T/16) waves x 16 queries; all key tiles (<= 2 x 64) of K and V staged once. Scores are
 // transposed as in attn_kernel (lane = one query, 16 keys per tile), and since every key is
@@ -313,6 +500,15 @@ hipError_t attention(bool bf16, bool causal, const u16* qkv, int64_t ldq, u16* o
       if (causal) attn_small_kernel<false, true><<<g2, b2, 0, s>>>(qkv, ldq, out, ldo, T, d);
       else attn_small_kernel<false, false><<<g2, b2, 0, s>>>(qkv, ldq, out, ldo, T, d);
     }
+    return hipGetLastError();
+  }
+  static const bool long32 = !getenv("CLM_ATTN_LONG") || atoi(getenv("CLM_ATTN_LONG")) != 0;
+  if (!causal && long32) {
+    const int nqb = (T + 127) / 128;
+    const int64_t nwg = (int64_t)nqb * H * B;
+    if (nwg > 0x7FFFFFFF) return hipErrorInvalidValue;
+    if (bf16) attn_long_kernel<true><<<(unsigned)nwg, 256, 0, s>>>(qkv, ldq, out, ldo, T, d, H, nqb);
+    else attn_long_kernel<false><<<(unsigned)nwg, 256, 0, s>>>(qkv, ldq, out, ldo, T, d, H, nqb);
     return hipGetLastError();
   }
   dim3 grid((T + 127) / 128, H, B), block(256);

@@ -65,6 +65,9 @@ def main(out_path, tmpdir):
         ref_txt = torch.cat([_renormalize(model.encode_ids(proc.token_ids(caps[a:a + 8]).cuda()))
                              for a in range(0, 37, 8)]).cpu()
         res["build_img_equal"] = bool(torch.equal(e_img.cpu(), ref_img))
+        dimg = (e_img.cpu().float() - ref_img.float()).abs()
+        res["build_img_maxdiff"] = float(dimg.max())
+        res["build_img_rows_differing"] = torch.nonzero(dimg.amax(1) > 0).flatten().tolist()
         res["build_txt_equal"] = bool(torch.equal(e_txt, ref_txt))
         res["file_equal"] = bool(torch.equal(obj["embeddings"], ref_txt))
         one = CosineIndex(dim, capacity=n)

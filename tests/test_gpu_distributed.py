@@ -34,7 +34,7 @@ def test_sharded_build_and_search_world2(tmp_path):
     assert r["file_rows_min_max"] == [37, 37]     # both ranks read the complete file
     for key in ("build_img_equal", "build_txt_equal", "file_equal", "search_idx_equal", "search_scores_equal",
                 "merge_roundtrip"):
-        assert r[key], key
+        assert r[key], (key, r)
     assert r["planted_top1"] == [5, 150_000, 150_001, 299_999]
 
 

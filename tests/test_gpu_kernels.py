@@ -131,13 +131,23 @@ def _attn_ref(qkv, B, T, H, causal):
 
 
 @pytest.mark.parametrize("dtype", ["bfloat16", "float16"])
-@pytest.mark.parametrize("B,T,H,causal", [(3, 50, 12, False), (2, 77, 8, True), (2, 77, 8, False),
-                                          (1, 577, 16, False), (2, 130, 2, True), (1, 1, 2, True)])
-def test_attention_vs_torch(dtype, B, T, H, causal):
+@pytest.mark.parametrize("B,T,H,causal,ramp", [(3, 50, 12, False, 0), (2, 77, 8, True, 0), (2, 77, 8, False, 0),
+                                               (1, 577, 16, False, 0), (2, 130, 2, True, 0), (1, 1, 2, True, 0),
+                                               (2, 130, 2, False, 0), (2, 160, 3, False, 0), (1, 193, 2, False, 0),
+                                               (2, 250, 4, False, 0), (1, 577, 2, False, 1), (1, 577, 2, False, -1),
+                                               (1, 700, 3, False, 1)])
+def test_attention_vs_torch(dtype, B, T, H, causal, ramp):
+    """T > 128 non-causal runs the 32x32x16 online-softmax kernel: tail tiles of 2 / 32 / 1 / 58
+    keys, and key magnitudes ramped up (the running max grows tile after tile: every rescale
+    fires) or down (none after the first tile)."""
     td = DT[dtype][0]
     g = torch.Generator(device="cuda").manual_seed(T * H)
     qkv = torch.randn((B * T, 3 * H * 64), generator=g, device="cuda")
     qkv[:, : H * 64] *= 0.125 * 3
+    if ramp:
+        t = torch.linspace(0.0, 1.0, T, device="cuda").repeat(B)
+        f = 0.5 + 2.0 * (t if ramp > 0 else 1.0 - t)
+        qkv[:, H * 64: 2 * H * 64] *= f[:, None]
     qkv = qkv.to(td)
     out = torch.full((B * T, H * 64 + 64), 7.0, device="cuda").to(td)
     C.check(C.lib().clm_attention(0, DT[dtype][1], int(causal), C.ptr(qkv), C.ptr(out), out.stride(0), B, T, H,
@@ -146,3 +156,90 @@ def test_attention_vs_torch(dtype, B, T, H, causal):
     err = (out[:, : H * 64].float() - ref).abs().max().item()
     assert err < (3e-2 if dtype == "bfloat16" else 4e-3), err
     assert (out[:, H * 64:].float() == 7.0).all()   # columns past d untouched
+
+
+def _rounding_probe(n, seed):
+    """fp32 values that stress the fp32 -> 16-bit RNE conversion: every binade from fp16
+    subnormals to past the fp16 overflow threshold, exact half-way ties, zero (acc + bias turns a -0 bias into +0, so none here)."""
+    g = np.random.default_rng(seed)
+    mag = np.exp2(g.uniform(-30, 18, n)).astype(np.float32)
+    v = (mag * g.choice([-1.0, 1.0], n)).astype(np.float32)
+    ties = (np.float32(1.0) + np.float32(2.0 ** -11) * (2 * g.integers(0, 1024, 64) + 1)).astype(np.float32)
+    v[:64] = ties                                   # half-way between two fp16 values
+    v[64:128] = (ties - 1.0) * np.float32(2.0 ** -14)   # ties in the fp16 subnormal range
+    v[128:136] = [0.0, -1e-30, 65504.0, 65519.0, 65520.0, -65520.0, 6e-8, -3e-8]
+    return torch.from_numpy(v)
+
+
+@pytest.mark.parametrize("dtype", ["bfloat16", "float16"])
+@pytest.mark.parametrize("N", [1024, 1023])
+def test_epilogue_rounding_matches_torch(dtype, N):
+    """A bias-only GEMM (A = W = 0) stores fp32 bias values through the 16-bit epilogue: the
+    packed 16-B path (N % 8 == 0) and the scalar tail path (N odd) round exactly as torch's
+    .to(dtype), in every tile configuration (batch invariance rests on this)."""
+    td = DT[dtype][0]
+    M, K = 80, 64
+    bias = _rounding_probe(N, N).cuda()
+    A = torch.zeros((M, K), dtype=td, device="cuda")
+    W = torch.zeros((N, K), dtype=td, device="cuda")
+    want = bias.to(td).view(torch.int16).expand(M, N)
+    for cfg in list(range(C.lib().clm_gemm_num_configs())) + [-1]:
+        out = torch.empty((M, N), dtype=td, device="cuda")
+        _gemm(dtype, C.CLM_EPI_STORE, cfg, A, W, out, bias=bias)
+        got = out.view(torch.int16)
+        bad = (got != want).nonzero()
+        assert bad.numel() == 0, (cfg, [(float(bias[j]), int(got[i, j]), int(want[i, j])) for i, j in bad[:4].tolist()])
+
+
+@pytest.mark.parametrize("dtype", ["bfloat16", "float16"])
+@pytest.mark.parametrize("epi", ["STORE", "GELU", "RESID"])
+def test_gemm_configs_bit_identical(dtype, epi):
+    """Every tile configuration computes each output row with the same K order and the same
+    epilogue arithmetic, so all give bit-identical results: the encoder's batch invariance
+    (a row's embedding does not depend on which batch, or which M tile, it lands in)."""
+    td = DT[dtype][0]
+    M, N, K = 300, 768, 768
+    g = torch.Generator(device="cuda").manual_seed(5)
+    A = torch.randn((M, K), generator=g, device="cuda").to(td)
+    W = (torch.randn((N, K), generator=g, device="cuda") / K ** 0.5).to(td)
+    bias = torch.randn(N, generator=g, device="cuda")
+    h0 = torch.randn((M, N), generator=g, device="cuda")
+    e = getattr(C, f"CLM_EPI_{epi}")
+    first = None
+    for cfg in range(C.lib().clm_gemm_num_configs()):
+        out = h0.clone() if epi == "RESID" else torch.empty((M, N), dtype=td, device="cuda")
+        _gemm(dtype, e, cfg, A, W, out, bias=bias)
+        if first is None:
+            first = out
+        else:
+            d = (out.float() - first.float()).abs()
+            assert torch.equal(out, first), (cfg, float(d.max()), d.amax(1).nonzero().flatten()[:8].tolist())
+
+
+@pytest.mark.parametrize("dtype", ["bfloat16", "float16"])
+@pytest.mark.parametrize("epi,N,K", [("STORE", 2304, 768), ("RESID", 768, 768), ("GELU", 3072, 768),
+                                     ("RESID", 768, 3072), ("STORE", 1536, 512), ("GELU", 2048, 512),
+                                     ("RESID", 512, 2048)])
+def test_gemm_rows_independent_of_batch(dtype, epi, N, K):
+    """The encoder's GEMM shapes at the heuristic config, run on row sets of different sizes
+    (a tower's M = batch x tokens, and the pruned last layer's M = batch): a row's output bits do
+    not depend on M or on where the row sits in its M tile."""
+    td = DT[dtype][0]
+    g = torch.Generator(device="cuda").manual_seed(N + K)
+    Mfull = 250
+    A = torch.randn((Mfull, K), generator=g, device="cuda").to(td)
+    W = (torch.randn((N, K), generator=g, device="cuda") / K ** 0.5).to(td)
+    bias = torch.randn(N, generator=g, device="cuda")
+    h0 = torch.randn((Mfull, N), generator=g, device="cuda")
+    e = getattr(C, f"CLM_EPI_{epi}")
+
+    def run(rows):
+        out = h0[rows].clone() if epi == "RESID" else torch.empty((len(rows), N), dtype=td, device="cuda")
+        _gemm(dtype, e, -1, A[rows].contiguous(), W, out, bias=bias)
+        return out
+
+    ref = run(list(range(Mfull)))
+    for rows in (list(range(200, 250)), list(range(150, 250)), [249, 3, 77, 200, 5], [249], list(range(50, 250))):
+        got = run(rows)
+        d = (got.float() - ref[rows].float()).abs()
+        assert torch.equal(got, ref[rows]), (len(rows), float(d.max()), d.amax(1).nonzero().flatten()[:8].tolist())
