@@ -95,6 +95,8 @@ def lib():
         "clm_gemm_num_configs": (c_int, []),
         "clm_debug_set": (None, [c_int]),
         "clm_attention": (c_int, [c_int, c_int, c_int, c_void_p, c_void_p, c_int64, c_int, c_int, c_int, c_void_p]),
+        "clm_layernorm": (c_int, [c_int, c_int, c_void_p, c_int64, c_int64, c_int, c_void_p, c_void_p, c_float, c_void_p,
+                                  c_int64, c_void_p]),
         "clm_prof_read": (c_int, [c_void_p, c_int, POINTER(ctypes.c_double), POINTER(ctypes.c_double),
                                   POINTER(c_int64)]),
     }
@@ -113,7 +115,7 @@ EXPORTED = (
     "clm_index_stats2",
     "clm_cosine_scores", "clm_topk_merge", "clm_l2_normalize", "clm_fuse_queries", "clm_last_error", "clm_version",
     "clm_model_desc_size", "clm_prof_enable", "clm_prof_read", "clm_gemm", "clm_gemm_num_configs",
-    "clm_attention", "clm_debug_set",
+    "clm_attention", "clm_layernorm", "clm_debug_set",
 )
 CLM_EPI_STORE, CLM_EPI_GELU, CLM_EPI_RESID, CLM_EPI_SCORE = 0, 1, 2, 4
 CLM_PROF_GEMM, CLM_PROF_ATTN, CLM_PROF_LN, CLM_PROF_OTHER = 0, 1, 2, 3

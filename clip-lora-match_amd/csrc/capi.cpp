@@ -756,6 +756,21 @@ int clm_attention(int hip_device, int dtype, int causal, const void* qkv, void* 
   return CLM_OK;
 }
 
+int clm_layernorm(int hip_device, int dtype, const float* src, int64_t lds, int64_t M, int d, const float* gamma,
+                  const float* beta, float eps, void* y, int64_t ldy, void* stream) {
+  if (dtype != CLM_BF16 && dtype != CLM_F16) return fail(CLM_E_ARG, "dtype must be bf16 or f16");
+  if (M < 0 || M > 0x7FFFFFFF || d <= 0 || d % 128 || d > 1024 || lds < d || ldy < d || (lds % 4) || (ldy % 4))
+    return fail(CLM_E_ARG, "bad shape");
+  if (M == 0) return CLM_OK;
+  DeviceGuard g(hip_device);
+  LnArgs a{};
+  a.mode = 0; a.src = src; a.lds = lds; a.hf = nullptr; a.ldh = 0;
+  a.g1 = gamma; a.b1 = beta; a.y = (u16*)y; a.ldy = ldy; a.M = (int)M; a.d = d; a.eps = eps;
+  hipError_t e = layernorm(dtype == CLM_BF16, a, (hipStream_t)stream);
+  if (e != hipSuccess) return fail(CLM_E_HIP, std::string("layernorm: ") + hipGetErrorString(e));
+  return CLM_OK;
+}
+
 int clm_prof_enable(clm_ctx* ctx, int enable) {
   if (!ctx) return fail(CLM_E_ARG, "null ctx");
   DeviceGuard g(ctx->dev);

@@ -68,27 +68,36 @@ __device__ __forceinline__ f32x4 mfma16(const u32x4& a, const u32x4& b, f32x4 c)
 }
 
 // ---- wave reductions (64 lanes) ---------------------------------------------
-__device__ __forceinline__ float wave_sum(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+// Butterfly all-reduce on the VALU: DPP quad_perm [1,0,3,2] / [2,3,0,1], row_half_mirror and
+// row_mirror inside each 16-lane row, then v_permlane16_swap / v_permlane32_swap across rows
+// (no ds_bpermute round trips through the LDS crossbar). Every lane combines the same two
+// partial values at every step (a + b == b + a), so all 64 lanes hold bit-identical results.
+template <int CTRL> __device__ __forceinline__ float dpp_f(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, 0xF, 0xF, false));
+}
+template <bool MAX> __device__ __forceinline__ float op2(float a, float b) { return MAX ? fmaxf(a, b) : a + b; }
+template <bool MAX> __device__ __forceinline__ float row16_reduce(float v) {
+  v = op2<MAX>(v, dpp_f<0xB1>(v));    // quad_perm [1,0,3,2]
+  v = op2<MAX>(v, dpp_f<0x4E>(v));    // quad_perm [2,3,0,1]
+  v = op2<MAX>(v, dpp_f<0x141>(v));   // row_half_mirror: the other quad of the 8
+  v = op2<MAX>(v, dpp_f<0x140>(v));   // row_mirror: the other 8 of the row
   return v;
 }
-__device__ __forceinline__ float wave_max(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
-  return v;
+// over the 4 lanes l, l ^ 16, l ^ 32, l ^ 48 (the 16-lane rows of a wave)
+template <bool MAX> __device__ __forceinline__ float cross_rows_reduce(float v) {
+  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  v = op2<MAX>(__uint_as_float(r[0]), __uint_as_float(r[1]));
+  const auto t = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return op2<MAX>(__uint_as_float(t[0]), __uint_as_float(t[1]));
 }
+template <bool MAX> __device__ __forceinline__ float wave_reduce(float v) {
+  return cross_rows_reduce<MAX>(row16_reduce<MAX>(v));
+}
+__device__ __forceinline__ float wave_sum(float v) { return wave_reduce<false>(v); }
+__device__ __forceinline__ float wave_max(float v) { return wave_reduce<true>(v); }
 // reductions inside aligned groups of 16 lanes (MFMA C-layout rows)
-__device__ __forceinline__ float group16_sum(float v) {
-#pragma unroll
-  for (int o = 8; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
-}
-__device__ __forceinline__ float group16_max(float v) {
-#pragma unroll
-  for (int o = 8; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
-  return v;
-}
+__device__ __forceinline__ float group16_sum(float v) { return row16_reduce<false>(v); }
+__device__ __forceinline__ float group16_max(float v) { return row16_reduce<true>(v); }
 
 __device__ __forceinline__ float quick_gelu(float x) {
   // TF/activations.py:123  x * sigmoid(1.702 x), as x * rcp(1 + 2^(-1.702 log2(e) x)):

@@ -9,7 +9,7 @@
 // Key tiles of 64: K and V staged in LDS row-major with the 128-B-row XOR swizzle (K read
 // as ds_read_b128 fragments, V through ds_read_b64_tr_b16, see v_frag_trT). Scores are
 // computed transposed, S^T = K Q^T, so each lane owns one query: the fp32 softmax reduces
-// in-lane plus two cross-lane steps, and P stays in registers as the B operand of
+// in-lane plus two cross-lane steps (v_permlane16/32_swap), and P stays in registers as the B operand of
 // O^T = V^T P^T. attn_kernel (T > 128) runs an online softmax over double-buffered tiles;
 // attn_small_kernel (T <= 128) holds every key and does one exact pass.
 #include "kernels.hpp"
@@ -139,8 +139,7 @@ __global__ __launch_bounds__(256, CAUSAL ? 2 : 3) void attn_kernel(const u16* qk
       for (int nb = 0; nb < 4; ++nb)
 #pragma unroll
         for (int j = 0; j < 4; ++j) tmax = fmaxf(tmax, sc[rb][nb][j]);
-      tmax = fmaxf(tmax, __shfl_xor(tmax, 16));
-      tmax = fmaxf(tmax, __shfl_xor(tmax, 32));
+      tmax = cross_rows_reduce<true>(tmax);
       const float mnew = fmaxf(mrow[rb], tmax * L2E);
       const float muse = mnew == -INFINITY ? 0.f : mnew;
       const float alpha = __builtin_amdgcn_exp2f(mrow[rb] - muse);
@@ -154,8 +153,7 @@ __global__ __launch_bounds__(256, CAUSAL ? 2 : 3) void attn_kernel(const u16* qk
           sc[rb][nb][j] = p;
           rs += p;
         }
-      rs += __shfl_xor(rs, 16);
-      rs += __shfl_xor(rs, 32);
+      rs = cross_rows_reduce<false>(rs);
       lrow[rb] = lrow[rb] * alpha + rs;
 #pragma unroll
       for (int nb = 0; nb < 4; ++nb)
@@ -446,8 +444,7 @@ __global__ __launch_bounds__(512) void attn_small_kernel(const u16* qkv, int64_t
       }
     }
   }
-  tmax = fmaxf(tmax, __shfl_xor(tmax, 16));
-  tmax = fmaxf(tmax, __shfl_xor(tmax, 32));
+  tmax = cross_rows_reduce<true>(tmax);
   const float m2 = tmax * L2E;   // key 0 is always visible: finite
   float rs = 0.f;
   f32x4 o[4];
@@ -476,8 +473,7 @@ __global__ __launch_bounds__(512) void attn_small_kernel(const u16* qkv, int64_t
 #pragma unroll
       for (int nb = 0; nb < 4; ++nb) o[nb] = mfma16<BF>(v_frag_trT(sV + kt * 8192, kk * 32, nb, lane), pb[kk], o[nb]);
   }
-  rs += __shfl_xor(rs, 16);
-  rs += __shfl_xor(rs, 32);
+  rs = cross_rows_reduce<false>(rs);
   if (qi >= T) return;
   const float inv = 1.0f / rs;
   u16* op = out + ((int64_t)b * T + qi) * ldo + h * 64 + 4 * g;

@@ -190,6 +190,11 @@ void clm_debug_set(int flags);
 /* attention over qkv [B*T, 3*H*64] (q pre-scaled), out [B*T, ldo] (device pointers) */
 int clm_attention(int hip_device, int dtype, int causal, const void* qkv, void* out, int64_t ldo,
                   int B, int T, int H, void* stream);
+/* LayerNorm of fp32 rows src [M, lds] over d columns (d a multiple of 128, <= 1024), eps, fp32
+ * gamma / beta -> y [M, ldy] in dtype CLM_BF16|CLM_F16 (device pointers); the encoder's kernel
+ * (TF/models/clip/modeling_clip.py:358,360 nn.LayerNorm) */
+int clm_layernorm(int hip_device, int dtype, const float* src, int64_t lds, int64_t M, int d,
+                  const float* gamma, const float* beta, float eps, void* y, int64_t ldy, void* stream);
 
 /* Kernel timing by category, measured with hipEvents recorded on the launch
  * stream around every kernel of clm_encode_* while enabled (adds event

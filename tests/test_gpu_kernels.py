@@ -243,3 +243,30 @@ def test_gemm_rows_independent_of_batch(dtype, epi, N, K):
         got = run(rows)
         d = (got.float() - ref[rows].float()).abs()
         assert torch.equal(got, ref[rows]), (len(rows), float(d.max()), d.amax(1).nonzero().flatten()[:8].tolist())
+
+
+def _ln(dtype, x, g, b, eps=1e-5):
+    M, d = x.shape
+    y = torch.empty((M, d), dtype=DT[dtype][0], device="cuda")
+    C.check(C.lib().clm_layernorm(0, DT[dtype][1], C.ptr(x), x.stride(0), M, d, C.ptr(g), C.ptr(b), eps, C.ptr(y),
+                                  y.stride(0), C.stream_of(x.device)), "clm_layernorm")
+    return y
+
+
+@pytest.mark.parametrize("dtype", ["bfloat16", "float16"])
+@pytest.mark.parametrize("d", [512, 768, 1024])
+def test_layernorm_vs_torch_and_row_invariant(dtype, d):
+    """The encoder LayerNorm kernel vs torch fp32 LayerNorm (one 16-bit rounding of the output
+    apart), and every row's bits independent of the row count and of the row's position (pairs of
+    rows share a wave)."""
+    g = torch.Generator(device="cuda").manual_seed(d)
+    M = 301
+    x = torch.randn((M, d), generator=g, device="cuda") * 3 + torch.randn((M, 1), generator=g, device="cuda") * 5
+    gam = torch.randn(d, generator=g, device="cuda")
+    bet = torch.randn(d, generator=g, device="cuda")
+    y = _ln(dtype, x, gam, bet)
+    ref = torch.nn.functional.layer_norm(x, (d,), gam, bet, 1e-5)
+    ulp = 2.0 ** (-8 if dtype == "bfloat16" else -11)
+    assert ((y.float() - ref).abs() <= ulp * ref.abs() + 1e-6).all()
+    for rows in ([300], [1, 0], list(range(1, 301)), [5, 6, 7], list(range(300, -1, -1))):
+        assert torch.equal(_ln(dtype, x[rows].contiguous(), gam, bet), y[rows]), rows
