@@ -1558,8 +1558,11 @@ int clm_topk_merge(int hip_device, const float* scores, const int64_t* idx, int6
   const bool out_d = is_device_ptr(out_scores) && is_device_ptr(out_idx);
   const size_t n_in = (size_t)nq * parts * k_in;
   uint8_t* w = nullptr;
-  const size_t bytes = (in_d ? 0 : n_in * 12) + (out_d ? 0 : (size_t)nq * k * 12) + 512;
-  if (bytes > 512 && hipMalloc(&w, bytes) != hipSuccess) { (void)hipGetLastError(); return fail(CLM_E_OOM, "workspace"); }
+  // every take() rounds its offset up to 256 B: size the workspace by the same rule (a flat
+  // +512 slack under-allocated 4 small takes -- found by the host-sanitizer harness)
+  const size_t bytes = (in_d ? 0 : round_up(n_in * 4, 256) + round_up(n_in * 8, 256)) +
+                       (out_d ? 0 : round_up((size_t)nq * k * 4, 256) + round_up((size_t)nq * k * 8, 256));
+  if (bytes > 0 && hipMalloc(&w, bytes) != hipSuccess) { (void)hipGetLastError(); return fail(CLM_E_OOM, "workspace"); }
   size_t off = 0;
   auto take = [&](size_t b) { size_t o = off; off = round_up(off + b, 256); return w + o; };
   const float* s_in = scores;

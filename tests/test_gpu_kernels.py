@@ -270,3 +270,16 @@ def test_layernorm_vs_torch_and_row_invariant(dtype, d):
     assert ((y.float() - ref).abs() <= ulp * ref.abs() + 1e-6).all()
     for rows in ([300], [1, 0], list(range(1, 301)), [5, 6, 7], list(range(300, -1, -1))):
         assert torch.equal(_ln(dtype, x[rows].contiguous(), gam, bet), y[rows]), rows
+
+
+def test_c_abi_under_host_sanitizers_with_device():
+    """The prebuilt host-sanitizer harness (csrc/Makefile `sanitize`, ASan + UBSan on the host
+    half) over the index lifecycle and the host-buffer entry points, results checked against
+    scalar host references inside the harness."""
+    import os
+    import subprocess
+    exe = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "clip-lora-match_amd", "host_check")
+    assert os.path.exists(exe), "build it with make -C clip-lora-match_amd/csrc sanitize"
+    p = subprocess.run([exe], capture_output=True, text=True, timeout=240)
+    assert p.returncode == 0, p.stdout[-3000:] + p.stderr[-3000:]
+    assert "argument + device checks, 0 failure(s)" in p.stdout

@@ -132,3 +132,24 @@ def test_no_device_fails_loudly():
     from clip_lora_match_amd.engine import ClipLoraModel
     with pytest.raises(RuntimeError):
         ClipLoraModel(clm.get_preset("tiny"))
+
+
+def _host_check():
+    """(re)build the host-sanitizer harness (csrc/Makefile `sanitize`: ASan + UBSan on the host
+    half of the C-ABI) and return its path"""
+    import subprocess
+    subprocess.run(["make", "-C", os.path.join(REPO, "clip-lora-match_amd", "csrc"), "sanitize"], check=True,
+                   capture_output=True, timeout=1200)
+    return os.path.join(REPO, "clip-lora-match_amd", "host_check")
+
+
+def test_c_abi_under_host_sanitizers():
+    """Every entry point's argument validation runs clean under ASan / UBSan (no device here: the
+    device half of the harness runs in tests/test_gpu_kernels.py)."""
+    import subprocess
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("a device is visible: the GPU test runs the full harness")
+    p = subprocess.run([_host_check()], capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0, p.stdout + p.stderr
+    assert "argument checks (no HIP device), 0 failure(s)" in p.stdout
