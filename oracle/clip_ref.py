@@ -25,7 +25,7 @@ What it restates (file:line into /root/reference unless prefixed TF/ =
 
 Parity status: pinned against goldens produced by transformers 5.15.0
 CLIPModel (the reference's own arithmetic) with the same synthetic weights --
-see tests/golden/make_golden.py and tests/test_oracle_golden.py.
+see tests/golden/make_golden.py and tests/test_oracle.py.
 """
 from __future__ import annotations
 

@@ -51,8 +51,11 @@ def test_random_strings_equal_transformers(pair):
     from hypothesis import given, settings, strategies as st
     ours, hf = pair
 
-    @settings(max_examples=300, deadline=None)
-    @given(st.text(alphabet=st.characters(codec="utf-8", exclude_categories=("Cs",)), max_size=60))
+    # assigned code points only (Python 3.10's Unicode 13 tables): an unassigned one, e.g.
+    # U+323B0, is a letter to one Unicode database and not to another (the regex module vs the
+    # tokenizers crate), which moves the pre-tokenizer split -- a version skew, not BPE
+    @settings(max_examples=300, deadline=None, derandomize=True)
+    @given(st.text(alphabet=st.characters(codec="utf-8", exclude_categories=("Cs", "Cn", "Co")), max_size=60))
     def check(t):
         assert ours(t, truncation=True, max_length=77)["input_ids"] == hf(t, truncation=True, max_length=77)["input_ids"]
     check()
