@@ -249,9 +249,11 @@ __device__ __forceinline__ u32x4 v_frag32(const uint8_t* tile, int k16, int dim0
 //     in the matching key order).
 // K / V tiles double-buffered in LDS, the next tile loaded into registers during this one's
 // MFMAs (one barrier per tile). Waves whose 32 queries all lie past T only stage tiles.
-template <bool BF>
-__global__ __launch_bounds__(256, 2) void attn_long_kernel(const u16* qkv, int64_t ldq, u16* out, int64_t ldo,
-                                                           int T, int d, int H, int nqb) {
+// SUB32: each 32-key half of the tile is its own online-softmax step (16 scores per lane live
+// instead of 32, so the kernel fits 128 VGPRs = 4 waves per SIMD; a half past T is skipped)
+template <bool BF, bool SUB32>
+__global__ __launch_bounds__(256, SUB32 ? 4 : 2) void attn_long_kernel(const u16* qkv, int64_t ldq, u16* out,
+                                                                       int64_t ldo, int T, int d, int H, int nqb) {
   constexpr float L2E = 1.4426950408889634f;
   __shared__ __attribute__((aligned(16))) uint8_t smem[2 * 16384];
   const int nwg = gridDim.x;
@@ -306,7 +308,59 @@ __global__ __launch_bounds__(256, 2) void attn_long_kernel(const u16* qkv, int64
   if (nkt > 1) load(1);
   __syncthreads();
   for (int kt = 0; kt < nkt; ++kt) {
-    if (active) {
+    if (SUB32 && active) {
+      const uint8_t* sK = smem + (kt & 1) * 16384;
+      const uint8_t* sV = sK + 8192;
+      const int kleft = T - kt * 64;   // valid keys in this tile (>= 1)
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb) {
+        if (kb * 32 >= kleft) break;   // wave-uniform
+        f32x16 sc;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) sc[r] = 0.f;
+        const int krow = kb * 32 + (lane & 31);
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          const u32x4 kf = *(const u32x4*)(sK + krow * 128 + swz(krow, 2 * s + hi) * 16);
+          sc = mfma32<BF>(kf, qf[s], sc);
+        }
+        if (kleft < kb * 32 + 32) {
+#pragma unroll
+          for (int r = 0; r < 16; ++r)
+            if (kb * 32 + 8 * (r >> 2) + 4 * hi + (r & 3) >= kleft) sc[r] = -INFINITY;
+        }
+        float tmax = sc[0];
+#pragma unroll
+        for (int r = 1; r < 16; ++r) tmax = fmaxf(tmax, sc[r]);
+        tmax = pair32_max(tmax);
+        const float mnew = fmaxf(m, tmax * L2E);   // finite: every processed half holds a valid key
+        if (__any(mnew > m)) {
+          const float alpha = __builtin_amdgcn_exp2f(m - mnew);
+          l *= alpha;
+#pragma unroll
+          for (int db = 0; db < 2; ++db)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) o[db][r] *= alpha;
+          m = mnew;
+        }
+        u32x4 pf[2];
+#pragma unroll
+        for (int hf = 0; hf < 2; ++hf) {
+          float p[8];
+#pragma unroll
+          for (int t = 0; t < 8; ++t) {
+            p[t] = __builtin_amdgcn_exp2f(fmaf(sc[8 * hf + t], L2E, -m));
+            l += p[t];
+          }
+          pf[hf] = u32x4{pack2<BF>(p[0], p[1]), pack2<BF>(p[2], p[3]), pack2<BF>(p[4], p[5]), pack2<BF>(p[6], p[7])};
+        }
+#pragma unroll
+        for (int hf = 0; hf < 2; ++hf)
+#pragma unroll
+          for (int db = 0; db < 2; ++db) o[db] = mfma32<BF>(v_frag32(sV, kb * 32 + 16 * hf, db * 32, lane), pf[hf], o[db]);
+      }
+    }
+    if (!SUB32 && active) {
       const uint8_t* sK = smem + (kt & 1) * 16384;
       const uint8_t* sV = sK + 8192;
       const int kleft = T - kt * 64;   // valid keys in this tile (>= 1)
@@ -388,16 +442,18 @@ __global__ __launch_bounds__(256, 2) void attn_long_kernel(const u16* qkv, int64
 // transposed as in attn_kernel (lane = one query, 16 keys per tile), and since every key is
 // resident the softmax is a single exact pass over <= 32 in-lane values: no online rescale,
 // P straight from registers into O^T = V^T P^T.
-template <bool BF, bool CAUSAL>
+// NT = key tiles held (1 for T <= 64: 16 KB of LDS per workgroup instead of 32, so twice as
+// many workgroups -- and their global loads -- are in flight per CU)
+template <bool BF, bool CAUSAL, int NT>
 __global__ __launch_bounds__(512) void attn_small_kernel(const u16* qkv, int64_t ldq, u16* out, int64_t ldo,
                                                          int T, int d) {
   constexpr float L2E = 1.4426950408889634f;
-  __shared__ __attribute__((aligned(16))) uint8_t smem[2 * 8192 + 2 * 8192];
+  __shared__ __attribute__((aligned(16))) uint8_t smem[NT * 8192 * 2];
   const int h = blockIdx.x, b = blockIdx.y;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, g = lane >> 4;
   const int nthr = blockDim.x;
-  uint8_t* sK = smem;                     // [2 tiles][64 keys][128 B] swizzled
-  uint8_t* sV = smem + 2 * 8192;          // [2 tiles][64 keys][128 B] swizzled, like sK
+  uint8_t* sK = smem;                     // [NT tiles][64 keys][128 B] swizzled
+  uint8_t* sV = smem + NT * 8192;         // [NT tiles][64 keys][128 B] swizzled, like sK
   const u16* base = qkv + (int64_t)b * T * ldq;
   const int ntiles = (T + 63) / 64;
   for (int ci = tid; ci < ntiles * 512; ci += nthr) {
@@ -421,10 +477,10 @@ __global__ __launch_bounds__(512) void attn_small_kernel(const u16* qkv, int64_t
   }
   __syncthreads();
   const int nkt = CAUSAL ? min((q0 + 15) / 64 + 1, ntiles) : ntiles;
-  f32x4 sc[2][4];   // S^T: lane holds query qi, keys kt*64 + nb*16 + 4g + 0..3
+  f32x4 sc[NT][4];   // S^T: lane holds query qi, keys kt*64 + nb*16 + 4g + 0..3
   float tmax = -INFINITY;
 #pragma unroll
-  for (int kt = 0; kt < 2; ++kt) {
+  for (int kt = 0; kt < NT; ++kt) {
     if (kt >= nkt) break;
     const uint8_t* tK = sK + kt * 8192;
 #pragma unroll
@@ -451,7 +507,7 @@ __global__ __launch_bounds__(512) void attn_small_kernel(const u16* qkv, int64_t
 #pragma unroll
   for (int nb = 0; nb < 4; ++nb) o[nb] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-  for (int kt = 0; kt < 2; ++kt) {
+  for (int kt = 0; kt < NT; ++kt) {
     if (kt >= nkt) break;
     u32x4 pb[2];
 #pragma unroll
@@ -489,22 +545,34 @@ hipError_t attention(bool bf16, bool causal, const u16* qkv, int64_t ldq, u16* o
   if (d != H * 64 || (ldq % 8) || (ldo % 8)) return hipErrorInvalidValue;
   if (T <= 128) {
     dim3 g2(H, B), b2(64 * ((T + 15) / 16));
+    // NT = 1 for T <= 64 measured no faster in the pipeline (0.46-0.48 ms of attention per step
+    // either way, pairs/s 0.7 % lower: profiles/r02_v4_attn_ab.txt), so both sizes hold 2 tiles
+    const bool one = false;
+#define CLM_SMALL(BFV, CV)                                                                    \
+    (one ? (attn_small_kernel<BFV, CV, 1><<<g2, b2, 0, s>>>(qkv, ldq, out, ldo, T, d), 0)     \
+         : (attn_small_kernel<BFV, CV, 2><<<g2, b2, 0, s>>>(qkv, ldq, out, ldo, T, d), 0))
     if (bf16) {
-      if (causal) attn_small_kernel<true, true><<<g2, b2, 0, s>>>(qkv, ldq, out, ldo, T, d);
-      else attn_small_kernel<true, false><<<g2, b2, 0, s>>>(qkv, ldq, out, ldo, T, d);
+      if (causal) CLM_SMALL(true, true); else CLM_SMALL(true, false);
     } else {
-      if (causal) attn_small_kernel<false, true><<<g2, b2, 0, s>>>(qkv, ldq, out, ldo, T, d);
-      else attn_small_kernel<false, false><<<g2, b2, 0, s>>>(qkv, ldq, out, ldo, T, d);
+      if (causal) CLM_SMALL(false, true); else CLM_SMALL(false, false);
     }
+#undef CLM_SMALL
     return hipGetLastError();
   }
-  static const bool long32 = !getenv("CLM_ATTN_LONG") || atoi(getenv("CLM_ATTN_LONG")) != 0;
-  if (!causal && long32) {
+  // $CLM_ATTN_LONG: 0 = the 16x16x32 attn_kernel, 1 = attn_long_kernel with 64-key softmax
+  // steps, 2 (default) = its SUB32 form (L/14: 6.53 vs 6.91 ms per step, profiles/r02_v4_attn_ab.txt)
+  static const int long_mode = getenv("CLM_ATTN_LONG") ? atoi(getenv("CLM_ATTN_LONG")) : 2;
+  if (!causal && long_mode) {
     const int nqb = (T + 127) / 128;
     const int64_t nwg = (int64_t)nqb * H * B;
     if (nwg > 0x7FFFFFFF) return hipErrorInvalidValue;
-    if (bf16) attn_long_kernel<true><<<(unsigned)nwg, 256, 0, s>>>(qkv, ldq, out, ldo, T, d, H, nqb);
-    else attn_long_kernel<false><<<(unsigned)nwg, 256, 0, s>>>(qkv, ldq, out, ldo, T, d, H, nqb);
+    if (long_mode == 2) {
+      if (bf16) attn_long_kernel<true, true><<<(unsigned)nwg, 256, 0, s>>>(qkv, ldq, out, ldo, T, d, H, nqb);
+      else attn_long_kernel<false, true><<<(unsigned)nwg, 256, 0, s>>>(qkv, ldq, out, ldo, T, d, H, nqb);
+    } else {
+      if (bf16) attn_long_kernel<true, false><<<(unsigned)nwg, 256, 0, s>>>(qkv, ldq, out, ldo, T, d, H, nqb);
+      else attn_long_kernel<false, false><<<(unsigned)nwg, 256, 0, s>>>(qkv, ldq, out, ldo, T, d, H, nqb);
+    }
     return hipGetLastError();
   }
   dim3 grid((T + 127) / 128, H, B), block(256);
