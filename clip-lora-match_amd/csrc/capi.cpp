@@ -999,6 +999,10 @@ static int pair_launch(clm_ctx* c, int split, hipEvent_t fork, const void* pixel
   const size_t pix_bytes = (size_t)d.image_size * d.image_size * d.channels * (layout == CLM_PIX_U8_HWC ? 1 : 4);
   const size_t out_row = (size_t)d.proj_dim * dtype_size(out_dtype);
   for (int i = 1; i < 2 * split; ++i) HIPCHK(hipStreamWaitEvent(c->ps[i], fork, 0));
+  struct Concurrent {   // tile heuristic hint for the duration of the launches (k_gemm.hip)
+    explicit Concurrent(bool on) { gemm_set_concurrent(on); }
+    ~Concurrent() { gemm_set_concurrent(false); }
+  } conc(n_img > 0 && n_txt > 0);
   for (int j = 0; j < split; ++j) {
     const int i0 = (int)((int64_t)n_img * j / split), i1 = (int)((int64_t)n_img * (j + 1) / split);
     const int t0 = (int)((int64_t)n_txt * j / split), t1 = (int)((int64_t)n_txt * (j + 1) / split);

@@ -229,12 +229,13 @@ hipError_t launch_id(int id, const GemmArgs& g, hipStream_t s) {
     case 11: case 12: case 13: case 14: case 15: case 16: case 17: case 18: case 19: case 20: case 21: case 22:
       return gemm2_launch(BF, EPI, id, g, s);
     case 23: return gemm3_launch(BF, EPI, g, s);
+    case 24: return launch_cfg<BF, EPI, 160, 128, 2, 2, 2>(g, s);
     default: return hipErrorInvalidValue;
   }
   }
 }
 
-constexpr int NCFG = 24;
+constexpr int NCFG = 25;
 
 // Tile choice: a cost model per kernel family, time(cfg) ~ rounds(cfg) x round_cost(cfg),
 // rounds = ceil(tiles / resident workgroups), round_cost = BM*BN*(workgroups per CU) /
@@ -254,14 +255,21 @@ constexpr int NCFG = 24;
 struct CfgModel { int id, bm, bn, wg_per_cu; double eff; };
 constexpr CfgModel MODELS_G2[] = {
   {15, 256, 192, 1, 2.569}, {16, 256, 128, 1, 2.349}, {17, 192, 256, 1, 2.521}, {18, 128, 256, 1, 2.340}};
+// 160x128 (config 24): the N = 512 / 768 RESID / PATCH shapes fill one round of 2-WG/CU slots
+// (480 / 496 tiles of 512, against 402 / 412 with 192x128): v_out 28.7 vs 32.0 µs, v_fc2 67.7
+// vs 74.9, t_out 24.0 vs 25.8, t_fc2 49.5 vs 53.7 (profiles/r02_v4_gemm_160x128.txt)
 constexpr CfgModel MODELS[] = {
   {0, 128, 128, 2, 0.975}, {4, 256, 256, 1, 1.18}, {6, 128, 192, 2, 0.955}, {7, 192, 128, 2, 0.955},
-  {8, 256, 128, 1, 1.025}, {10, 128, 256, 1, 1.056}};
+  {8, 256, 128, 1, 1.025}, {10, 128, 256, 1, 1.056}, {24, 160, 128, 2, 0.93}};
+thread_local bool g_concurrent = false;
 template <int NM>
 int pick_from(const CfgModel (&models)[NM], int M, int N) {
+  static const long long env_skip = getenv("CLM_GEMM_SKIP_MASK") ? atoll(getenv("CLM_GEMM_SKIP_MASK")) : 0;   // A/B: bit per config id
+  const long long skip = env_skip | (g_concurrent ? (1LL << 24) : 0);
   int best = models[0].id;
   double best_cost = 1e300;
   for (const CfgModel& c : models) {
+    if ((skip >> c.id) & 1) continue;
     const int64_t tiles = (int64_t)((M + c.bm - 1) / c.bm) * ((N + c.bn - 1) / c.bn);
     const int64_t slots = 256LL * c.wg_per_cu;
     const int64_t rounds = (tiles + slots - 1) / slots;
@@ -334,6 +342,8 @@ hipError_t gemm_cfg(bool bf16, int epi, int config, const GemmArgs& g, hipStream
 }
 
 hipError_t gemm(bool bf16, int epi, const GemmArgs& g, hipStream_t s) { return gemm_cfg(bf16, epi, -1, g, s); }
+
+void gemm_set_concurrent(bool on) { g_concurrent = on; }
 
 
 }  // namespace clm

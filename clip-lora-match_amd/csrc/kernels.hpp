@@ -52,6 +52,11 @@ hipError_t gemm(bool bf16, int epi, const GemmArgs& g, hipStream_t s);
 // explicit tile configuration (config < 0: heuristic); configs: k_gemm.hip launch_id
 hipError_t gemm_cfg(bool bf16, int epi, int config, const GemmArgs& g, hipStream_t s);
 int gemm_num_configs();
+// host-side hint for the tile heuristic of the calling thread: true while two towers are being
+// launched on concurrent streams (clm_encode_pair). Then the RESID / PATCH GEMMs keep the
+// 192x128 / 128x192 tiles, whose single round leaves ~20 % of the workgroup slots to the
+// other stream; alone, the slot-filling 160x128 tiles are faster (profiles/r02_v4_gemm_160x128.txt)
+void gemm_set_concurrent(bool on);
 
 // ----------------------------------------------------------- row ops -------
 // LayerNorm over rows of a fp32 matrix, one wave per row.

@@ -21,7 +21,7 @@ for name, (M, N, K, epi) in SHAPES.items():
     W = ((torch.rand((N, K), device=dev) * 2 - 1) / K ** 0.5).to(torch.bfloat16)
     out = torch.zeros((M, N), device=dev, dtype=torch.float32 if epi == 2 else torch.bfloat16)
     bias = torch.zeros(N, device=dev)
-    for cfg in (-1, 4):
+    for cfg in [int(c) for c in os.environ.get("AB_CFGS", "-1,4").split(",")]:
         for dbg in (0, 1):
             L.clm_debug_set(dbg)
             run = lambda: C.check(L.clm_gemm(0, C.CLM_BF16, epi, cfg, C.ptr(A), K, C.ptr(W), K, M, N, K, C.ptr(out), N,
