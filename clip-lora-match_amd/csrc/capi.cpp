@@ -556,6 +556,17 @@ bool prune_last_layer() {
   return v == 1 && !(g_gemm_debug & 8);   // clm_debug_set bit 8: every row (tests)
 }
 
+// q/k/v projection + attention fused into one launch for T <= 128 (k_gemm_attn.hip) unless
+// $CLM_FUSED_ATTN=0 or clm_debug_set bit 16 (tests: the two-kernel path, bit-identical)
+bool fused_attention(int T, int H, int d, int K) {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("CLM_FUSED_ATTN");
+    v = (e && !atoi(e)) ? 0 : 1;
+  }
+  return v == 1 && !(g_gemm_debug & 16) && gemm_attn_supported(T, H, d, K);
+}
+
 // encoder layers on the residual stream T.h; the first layer's LN1 output must already be in T.X.
 // Returns with the pooled rows in T.hc (pruned: *pooled_rows = true) or all rows in T.h.
 // ln_fold: the residual GEMMs (out_proj, fc2) also write the 16-bit residual copy into T.X and
@@ -589,9 +600,15 @@ int run_layers(clm_ctx* c, Tower& T, int B, int S, bool causal, const int32_t* i
     } else {
       g.W = Lw.w_qkv; g.ldw = Lw.k_qkv; g.bias = Lw.b_qkv;
     }
-    { PROF(CLM_PROF_GEMM, 2.0 * M * g.N * g.K); KCHK(gemm(bf, g.lnstat ? EPI_STORE_LN : EPI_STORE, g, st)); }
-    { PROF(CLM_PROF_ATTN, 4.0 * B * T.H * (double)S * S * 64);
-      KCHK(attention(bf, causal, T.QKV, 3 * T.d, T.O, T.ldo, B, S, T.H, T.d, st)); }
+    if (!g.lnstat && fused_attention(S, T.H, T.d, g.K)) {
+      // one launch: the q/k/v GEMM's tiles attend their own sequences (GEMM + attention FLOPs)
+      PROF(CLM_PROF_GEMM, 2.0 * M * g.N * g.K + 4.0 * B * T.H * (double)S * S * 64);
+      KCHK(gemm_attn(bf, causal, g.A, g.lda, g.W, g.ldw, g.bias, T.O, T.ldo, B, S, T.H, T.d, g.K, st));
+    } else {
+      { PROF(CLM_PROF_GEMM, 2.0 * M * g.N * g.K); KCHK(gemm(bf, g.lnstat ? EPI_STORE_LN : EPI_STORE, g, st)); }
+      { PROF(CLM_PROF_ATTN, 4.0 * B * T.H * (double)S * S * 64);
+        KCHK(attention(bf, causal, T.QKV, 3 * T.d, T.O, T.ldo, B, S, T.H, T.d, st)); }
+    }
     float* h = T.h;
     u16* O = T.O;
     const bool pooled = prune && last;

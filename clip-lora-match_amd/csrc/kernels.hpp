@@ -111,6 +111,11 @@ hipError_t pool_project(const float* h, int64_t ldh, int B, int T, int d, const 
 // qkv [B*T, 3d] (q pre-scaled by head_dim^-0.5), out [B*T, ldo] compute dtype.
 hipError_t attention(bool bf16, bool causal, const u16* qkv, int64_t ldq, u16* out, int64_t ldo,
                      int B, int T, int H, int d, hipStream_t s);
+// fused q/k/v projection + attention (k_gemm_attn.hip), T <= 128: out = attention(X . Wqkv^T +
+// bias) without materialising QKV; bit-identical to gemm(EPI_STORE) + attention()
+bool gemm_attn_supported(int T, int H, int d, int K);
+hipError_t gemm_attn(bool bf16, bool causal, const u16* X, int64_t ldx, const u16* W, int64_t ldw, const float* bias,
+                     u16* out, int64_t ldo, int B, int T, int H, int d, int K, hipStream_t s);
 
 // ----------------------------------------------------------- search --------
 // rows f32|f16 [n, dim] -> fp16 dst + fp32 inverse norms of the fp16-rounded rows

@@ -246,3 +246,29 @@ def test_ln_fold_matches_layernorm_kernels(dtype, monkeypatch):
         _check(outs[fold][0], outs[fold][1], g["emb_img"], g["emb_txt"], dtype)
         m.close()
     _check(outs["1"][0], outs["1"][1], outs["0"][0], outs["0"][1], dtype)
+
+
+@pytest.mark.parametrize("preset,dtype,mode", [("tiny", "float16", "merged"), ("tiny", "bfloat16", "unmerged"),
+                                               ("ViT-B/32", "bfloat16", "merged"), ("ViT-B/32", "float16", "merged"),
+                                               ("ViT-B/32", "bfloat16", "unmerged")])
+def test_fused_qkv_attention_bit_identical(preset, dtype, mode):
+    """T <= 128: the q/k/v GEMM and the attention run as ONE kernel (k_gemm_attn.hip, a tile =
+    256 / T whole sequences x one head). Its q/k/v values are rounded exactly as the STORE
+    epilogue rounds them and attended with attn_small_kernel's arithmetic, so the embeddings
+    equal the two-kernel path (clm_debug_set bit 16) bit for bit: ragged batch sizes (partial
+    last tile), ragged caption lengths (tiles of 256 // L captions), causal text."""
+    from clip_lora_match_amd import _capi as C
+    m, cfg, sd, lora = _model(preset, dtype, mode, max_batch=40)
+    imgs = torch.from_numpy(syn.images_u8(37, cfg.image_size, 21)).cuda()
+    ids = syn.captions(37, cfg.max_pos, cfg.bos_token_id, cfg.eos_token_id, 22)
+    cases = [torch.from_numpy(ids).cuda(), torch.from_numpy(ids[:11, :13].copy()).cuda(),
+             torch.from_numpy(ids[:3, :5].copy()).cuda()]
+    outs = {}
+    try:
+        for flag in (0, 16):
+            C.lib().clm_debug_set(flag)
+            outs[flag] = [m.encode_pixels(imgs), m.encode_pixels(imgs[:1])] + [m.encode_ids(x) for x in cases]
+    finally:
+        C.lib().clm_debug_set(0)
+    for i, (a, b) in enumerate(zip(outs[0], outs[16])):
+        assert torch.equal(a, b), f"case {i}: fused vs two-kernel max diff {(a - b).abs().max().item():.3e}"
