@@ -589,6 +589,25 @@ int run_layers(clm_ctx* c, Tower& T, int B, int S, bool causal, const int32_t* i
       KCHK(ln_finalize(T.stats, T.d / 32, (int)M, c->desc.ln_eps, T.lnst, st)); }
     return CLM_OK;
   };
+  // the pruned last layer's residual GEMMs have only B (pooled) rows: K is split into slices of
+  // >= 4 K-steps (a fixed count per shape, so a row's bits do not depend on B), partials in the
+  // QKV workspace, which is idle by then (B * S rows * 3d 16-bit values)
+  static const bool pooled_small = !(getenv("CLM_POOLED_SPLITK") && !atoi(getenv("CLM_POOLED_SPLITK")));   // A/B switch
+  auto pooled_resid = [&](GemmArgs& g) -> int {
+    if (!pooled_small) {
+      PROF(CLM_PROF_GEMM, 2.0 * g.M * g.N * g.K);
+      KCHK(gemm(bf, EPI_RESID, g, st));
+      return CLM_OK;
+    }
+    const int nk = g.K / 64;
+    int slices = 1;
+    for (int sl = nk / 4; sl >= 2; --sl)
+      if (nk % sl == 0 && gemm_splitk_ws_bytes(1, g.N, sl) <= (size_t)S * 3 * T.d * 2) { slices = sl; break; }
+    PROF(CLM_PROF_GEMM, 2.0 * g.M * g.N * g.K);
+    if (slices > 1) KCHK(gemm_splitk_resid(bf, g, slices, (float*)T.QKV, st));
+    else KCHK(gemm_cfg(bf, EPI_RESID, 5, g, st));
+    return CLM_OK;
+  };
   for (int l = 0; l < T.L; ++l) {
     LayerW& Lw = T.layers[l];
     const bool last = l + 1 == T.L;
@@ -632,7 +651,12 @@ int run_layers(clm_ctx* c, Tower& T, int B, int S, bool causal, const int32_t* i
       int r = resid_stats(g, M);
       if (r) return r;
     } else {
-      { PROF(CLM_PROF_GEMM, 2.0 * M * g.N * g.K); KCHK(gemm(bf, EPI_RESID, g, st)); }
+      if (pooled) {
+        int r = pooled_resid(g);
+        if (r) return r;
+      } else {
+        PROF(CLM_PROF_GEMM, 2.0 * M * g.N * g.K); KCHK(gemm(bf, EPI_RESID, g, st));
+      }
       PROF(CLM_PROF_LN, (double)M * T.d * 6.0);
       KCHK(layernorm(bf, ln_into_x(c, T, M, Lw.ln2_g, Lw.ln2_b, Lw.a_fc1, Lw.r_fc1, h), st));
     }
@@ -643,7 +667,8 @@ int run_layers(clm_ctx* c, Tower& T, int B, int S, bool causal, const int32_t* i
     } else {
       g.W = Lw.w_fc1; g.ldw = Lw.k_fc1; g.bias = Lw.b_fc1;
     }
-    { PROF(CLM_PROF_GEMM, 2.0 * M * g.N * g.K); KCHK(gemm(bf, g.lnstat ? EPI_GELU_LN : EPI_GELU, g, st)); }
+    { PROF(CLM_PROF_GEMM, 2.0 * M * g.N * g.K);   // pooled rows: 64 x 128 tiles (config 5) fill the chip
+      KCHK(pooled && pooled_small ? gemm_cfg(bf, EPI_GELU, 5, g, st) : gemm(bf, g.lnstat ? EPI_GELU_LN : EPI_GELU, g, st)); }
     if (Lw.r_fc2) { PROF(CLM_PROF_OTHER, 2.0 * M * T.mlp + 4.0 * Lw.r_fc2 * T.mlp);
       KCHK(lora_down(bf, T.Hm, T.ldm, (int)M, T.mlp, Lw.a_fc2, Lw.r_fc2, RPAD, st)); }
     g = GemmArgs{};
@@ -653,7 +678,12 @@ int run_layers(clm_ctx* c, Tower& T, int B, int S, bool causal, const int32_t* i
       int r = resid_stats(g, M);
       if (r) return r;
     } else {
-      { PROF(CLM_PROF_GEMM, 2.0 * M * g.N * g.K); KCHK(gemm(bf, EPI_RESID, g, st)); }
+      if (pooled) {
+        int r = pooled_resid(g);
+        if (r) return r;
+      } else {
+        PROF(CLM_PROF_GEMM, 2.0 * M * g.N * g.K); KCHK(gemm(bf, EPI_RESID, g, st));
+      }
       if (!last) {
         LayerW& Ln = T.layers[l + 1];
         PROF(CLM_PROF_LN, (double)M * T.d * 6.0);

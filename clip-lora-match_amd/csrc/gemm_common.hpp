@@ -99,7 +99,7 @@ __device__ __forceinline__ void epilogue_scalar(const GemmArgs& g, const f32x4 (
 // Epilogue of one BM x BN tile from the accumulators.
 template <bool BF, int EPI, int BM, int BN, int WM, int WN, int STAGES>
 __device__ __forceinline__ void epilogue(const GemmArgs& g, const f32x4 (&acc)[BM / WM / 16][BN / WN / 16], int m0,
-                                         int n0, int wm, int wn, int lane) {
+                                         int n0, int wm, int wn, int lane, int64_t out_off = 0) {
   using C = Cfg<BM, BN, WM, WN, STAGES>;
   // lane owns C[m, n..n+3], m = wrow + 16*mb, n = wcol + 16*nb.
   // Every global load of the epilogue (bias / cscale / row scales, residual, pos rows) is
@@ -312,7 +312,7 @@ __device__ __forceinline__ void epilogue(const GemmArgs& g, const f32x4 (&acc)[B
       if constexpr (EPI == EPI_FILTER) th[mb] = m < g.M ? g.theta[(int64_t)m * g.theta_ld] : 0.f;
     }
     if constexpr (EPI == EPI_SCORE) {
-      const auto ob = buf_rsrc((const float*)g.out + (int64_t)m0 * g.ldo, nrec);
+      const auto ob = buf_rsrc((const float*)g.out + out_off + (int64_t)m0 * g.ldo, nrec);
 #pragma unroll
       for (int mb = 0; mb < C::TM; ++mb) {
         const int m = wrow + mb * 16;

@@ -41,14 +41,20 @@ __global__ __launch_bounds__(WM * WN * 64, (Cfg<BM, BN, WM, WN, STAGES>::WAVES_P
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int ntn = (g.N + BN - 1) / BN, ntm = (g.M + BM - 1) / BM;
-  const int ntiles = ntn * ntm, G = gridDim.x;
+  const int ks = g.ksplit > 1 ? g.ksplit : 1;   // split-K: work unit = (tile, K slice)
+  const int ntiles = ntn * ntm * ks, G = gridDim.x;
   const int xb = xcd_remap(blockIdx.x, G);
   const int n_my = (ntiles - 1 - xb) / G + 1;
-  const int nk = g.K / BK;
+  const int nk = g.K / BK / ks;
   const int S = n_my * nk;   // K-steps of all this workgroup's tiles, one ring
 
-  auto coords = [&](int i, int& m0, int& n0) {
-    const int t = i * G + xb;
+  auto coords = [&](int i, int& m0, int& n0, int& k0) {
+    int t = i * G + xb;
+    k0 = 0;
+    if (ks > 1) {   // the slices of one tile are adjacent units (same XCD under the remap)
+      k0 = (t % ks) * nk * BK;
+      t /= ks;
+    }
     int tm, tn;
     if (g.m_fastest) {          // every query tile of one index tile back to back (search)
       tm = t % ntm;
@@ -72,17 +78,17 @@ __global__ __launch_bounds__(WM * WN * 64, (Cfg<BM, BN, WM, WN, STAGES>::WAVES_P
   const u16* a_src[C::LA];
   const u16* w_src[C::LB];
   auto point = [&](int i) {
-    int m0, n0;
-    coords(i, m0, n0);
+    int m0, n0, k0;
+    coords(i, m0, n0, k0);
 #pragma unroll
     for (int j = 0; j < C::LA; ++j) {
       const int row = (wid * C::LA + j) * 8 + r8;
-      a_src[j] = g.A + (int64_t)min(m0 + row, g.M - 1) * g.lda + (pc ^ ((row >> 1) & 7)) * 8;
+      a_src[j] = g.A + (int64_t)min(m0 + row, g.M - 1) * g.lda + k0 + (pc ^ ((row >> 1) & 7)) * 8;
     }
 #pragma unroll
     for (int j = 0; j < C::LB; ++j) {
       const int row = (wid * C::LB + j) * 8 + r8;
-      w_src[j] = g.W + (int64_t)min(n0 + row, g.N - 1) * g.ldw + (pc ^ ((row >> 1) & 7)) * 8;
+      w_src[j] = g.W + (int64_t)min(n0 + row, g.N - 1) * g.ldw + k0 + (pc ^ ((row >> 1) & 7)) * 8;
     }
   };
   int ld_i = 0, ld_kt = 0;
@@ -118,8 +124,8 @@ __global__ __launch_bounds__(WM * WN * 64, (Cfg<BM, BN, WM, WN, STAGES>::WAVES_P
   constexpr int E0 = epi_min_stores<EPI, C::TM, C::TN>();
   constexpr int E = E0 + C::L * (STAGES - 2) > 63 ? 63 - C::L * (STAGES - 2) : E0;   // 6-bit vmcnt: over-wait
   const bool vec_epi = (g.N % 4) == 0 && (g.ldo % 4) == 0 && !(g.debug & 1);
-  int c_i = 0, c_kt = 0, m0, n0;
-  coords(0, m0, n0);
+  int c_i = 0, c_kt = 0, m0, n0, k0;
+  coords(0, m0, n0, k0);
   int since_end = STAGES;   // K-steps since the last tile end
   for (int s = 0; s < S; ++s) {
     // retire K-step s's DMA, leaving younger ones in flight: the STAGES-2 later K-steps' DMA
@@ -166,14 +172,15 @@ __global__ __launch_bounds__(WM * WN * 64, (Cfg<BM, BN, WM, WN, STAGES>::WAVES_P
 #pragma unroll
           for (int nb = 0; nb < C::TN; ++nb) asm volatile("" ::"v"(acc[mb][nb]));
       } else {
-        epilogue<BF, EPI, BM, BN, WM, WN, STAGES>(g, acc, m0, n0, wm, wn, lane);
+        epilogue<BF, EPI, BM, BN, WM, WN, STAGES>(g, acc, m0, n0, wm, wn, lane,
+                                                  ks > 1 ? (int64_t)(k0 / (nk * BK)) * g.split_stride : 0);
       }
 #pragma unroll
       for (int i = 0; i < C::TM; ++i)
 #pragma unroll
         for (int j = 0; j < C::TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
       c_kt = 0;
-      if (++c_i < n_my) coords(c_i, m0, n0);
+      if (++c_i < n_my) coords(c_i, m0, n0, k0);
     }
   }
 }
@@ -200,7 +207,7 @@ hipError_t launch_cfg(const GemmArgs& g, hipStream_t s) {
     (void)hipGetLastError();
     sl = per_cu * cus;
   }
-  const int tiles = ((g.N + BN - 1) / BN) * ((g.M + BM - 1) / BM);
+  const int tiles = ((g.N + BN - 1) / BN) * ((g.M + BM - 1) / BM) * (g.ksplit > 1 ? g.ksplit : 1);
   const int nwg = (g.debug & 4) ? tiles : std::min(tiles, std::max(1, sl * grid_pct() / 100));   // debug bit 2: one tile per workgroup
   kern<<<dim3(nwg), dim3(C::NT), C::LDS, s>>>(g);
   return hipGetLastError();
@@ -341,7 +348,47 @@ hipError_t gemm_cfg(bool bf16, int epi, int config, const GemmArgs& g, hipStream
   return bf16 ? dispatch<true>(epi, id, g, s) : dispatch<false>(epi, id, g, s);
 }
 
-hipError_t gemm(bool bf16, int epi, const GemmArgs& g, hipStream_t s) { return gemm_cfg(bf16, epi, -1, g, s); }
+hipError_t gemm(bool bf16, int epi, const GemmArgs& g, hipStream_t s) {
+  if (g.ksplit > 1) return hipErrorInvalidValue;   // split-K: gemm_splitk_resid only
+  return gemm_cfg(bf16, epi, -1, g, s);
+}
+
+namespace {
+// out[m, n] += sum_s ws[s][m][n] (slice order) + bias[n]: the RESID epilogue's arithmetic,
+// h + (acc + bias), with acc summed over the K slices; 4 columns per thread
+__global__ __launch_bounds__(256) void splitk_resid_kernel(const float* ws, int slices, int M, int N, const float* bias,
+                                                          float* out, int64_t ldo) {
+  const int n4 = N / 4;
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (int64_t)M * n4) return;
+  const int m = (int)(i / n4), n = (int)(i - (int64_t)m * n4) * 4;
+  const int64_t stride = (int64_t)M * N;
+  float4 acc = *(const float4*)(ws + (int64_t)m * N + n);
+  for (int s = 1; s < slices; ++s) {
+    const float4 p = *(const float4*)(ws + s * stride + (int64_t)m * N + n);
+    acc.x += p.x; acc.y += p.y; acc.z += p.z; acc.w += p.w;
+  }
+  const float4 b = bias ? *(const float4*)(bias + n) : make_float4(0.f, 0.f, 0.f, 0.f);
+  float4* o = (float4*)(out + (int64_t)m * ldo + n);
+  float4 h = *o;
+  h.x = h.x + (acc.x + b.x); h.y = h.y + (acc.y + b.y); h.z = h.z + (acc.z + b.z); h.w = h.w + (acc.w + b.w);
+  *o = h;
+}
+}  // namespace
+
+hipError_t gemm_splitk_resid(bool bf16, const GemmArgs& g, int slices, float* ws, hipStream_t s) {
+  if (g.M <= 0 || g.N <= 0) return hipSuccess;
+  if (slices < 1 || g.K <= 0 || g.K % (BK * slices) || (g.N % 4) || (g.ldo % 4) || !ws) return hipErrorInvalidValue;
+  GemmArgs p = g;   // slice partials: EPI_SCORE with no scales stores acc * 1 * 1 = acc exactly
+  p.out = ws; p.ldo = g.N; p.bias = nullptr; p.rscale = nullptr; p.cscale = nullptr;
+  p.ksplit = slices; p.split_stride = (int64_t)g.M * g.N;
+  // 64 x 128 tiles (config 5): the few rows still spread over many workgroups
+  hipError_t e = gemm_cfg(bf16, EPI_SCORE, 5, p, s);
+  if (e != hipSuccess) return e;
+  const int64_t n = (int64_t)g.M * (g.N / 4);
+  splitk_resid_kernel<<<(unsigned)((n + 255) / 256), 256, 0, s>>>(ws, slices, g.M, g.N, g.bias, (float*)g.out, g.ldo);
+  return hipGetLastError();
+}
 
 void gemm_set_concurrent(bool on) { g_concurrent = on; }
 

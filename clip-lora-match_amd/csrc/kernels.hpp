@@ -44,11 +44,20 @@ struct GemmArgs {
   u16* hb; int64_t ldhb; float2* stats;
   const float2* lnstat; const float* cvec;
   int m_fastest;   // tile order: 1 = consecutive workgroups walk M (share one W tile)
+  // split-K (gemm_kernel configs only, EPI_SCORE as the fp32 partial store): ksplit > 1 cuts K
+  // into ksplit equal slices; slice s of every tile writes out + s * split_stride
+  int ksplit; int64_t split_stride;
   int debug;       // diagnostics only: 1 = skip the epilogue (accumulators kept live), 2 = drop its
                    // stores, 4 = one tile per workgroup (non-persistent grid)
 };
 
 hipError_t gemm(bool bf16, int epi, const GemmArgs& g, hipStream_t s);
+// Few-row residual GEMM (the pruned last layer: M = pooled rows): out[m,n] += acc + bias with K cut
+// into `slices` (deterministic: the fp32 partials [slices][M][N] go to ws and are summed in slice
+// order by one reduce kernel, so a row's result does not depend on M). slices must divide K / 64.
+hipError_t gemm_splitk_resid(bool bf16, const GemmArgs& g, int slices, float* ws, hipStream_t s);
+// fp32 workspace bytes gemm_splitk_resid needs
+inline size_t gemm_splitk_ws_bytes(int M, int N, int slices) { return (size_t)slices * M * N * 4; }
 // explicit tile configuration (config < 0: heuristic); configs: k_gemm.hip launch_id
 hipError_t gemm_cfg(bool bf16, int epi, int config, const GemmArgs& g, hipStream_t s);
 int gemm_num_configs();

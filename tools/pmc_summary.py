@@ -8,6 +8,8 @@ gfx950 corrections (MI355X_MICROARCH.md §HBM, § Per-instruction cycle constant
     over the 8 XCDs -> kernel cycles = GRBM_GUI_ACTIVE / 8, and
     mfma_busy_frac = MFMA_BUSY / (kernel cycles * 256 CUs * 4 SIMDs).
   * SQ_INSTS_VALU_MFMA_MOPS_BF16 counts 512-FLOP units -> MFMA FLOPs = 512 * MOPS.
+  * l2_hit_rate = TCC_HIT_sum / (TCC_HIT_sum + TCC_MISS_sum) (the XCD L2s; a miss is served by
+    the Infinity Cache or HBM).
 GEMM launches are labelled by their position in the sequential encode step (tools/pmc.sh runs
 bench.py --sequential): vision patch, 12 x (qkv, out, fc1, fc2), then text 12 x (qkv, out, fc1,
 fc2); the last layer's out / fc1 / fc2 run on the pooled rows only.
@@ -29,7 +31,8 @@ def short(name):
     m = re.search(r"(gemm2?_kernel)<([^>]*)>", name)
     if m:
         return m.group(1) + "<" + m.group(2) + ">"
-    return re.sub(r"\(.*", "", name).replace("clm::(anonymous namespace)::", "").replace("void ", "")
+    name = name.replace("clm::(anonymous namespace)::", "").replace("void ", "")
+    return re.sub(r"\(.*", "", name)
 
 
 def step_labels(layers_v=12, layers_t=12):
@@ -94,6 +97,8 @@ def main(src="gpurun_out/pmc", tag="r02"):
             o["mfma_flops"] = 512 * m["SQ_INSTS_VALU_MFMA_MOPS_BF16"]
         if "SQ_LDS_BANK_CONFLICT" in m and m.get("SQ_INSTS_LDS"):
             o["lds_bank_conflicts_per_lds_inst"] = m["SQ_LDS_BANK_CONFLICT"] / m["SQ_INSTS_LDS"]
+        if m.get("TCC_HIT_sum") is not None and m.get("TCC_MISS_sum") is not None and m["TCC_HIT_sum"] + m["TCC_MISS_sum"]:
+            o["l2_hit_rate"] = m["TCC_HIT_sum"] / (m["TCC_HIT_sum"] + m["TCC_MISS_sum"])
         o["launches"] = max(len(v) for v in cv.values())
         return o
 
