@@ -503,7 +503,8 @@ def main():
         "embeds_per_s": round(2 * pairs_s, 1),
         "step_tflops_per_gpu": round(step_flops / (ms_step * 1e-3) / 1e12, 2),
         "roofline": {
-            "kernel": "gemm_kernel / gemm2_kernel (MFMA 16x16x32, all encoder GEMMs)",
+            "kernel": "gemm_kernel / gemm2_kernel / gemm_attn_kernel (MFMA 16x16x32: every encoder GEMM; "
+                      "the q/k/v GEMM fused with its attention, whose FLOPs it counts)",
             "bound": "mfma",
             "achieved": round(gemm_flops / (gemm_ms * 1e-3) / 1e12, 2),
             "peak": MFMA_PEAK_TFLOPS,

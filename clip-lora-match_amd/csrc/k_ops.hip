@@ -384,16 +384,17 @@ __global__ __launch_bounds__(64) void gather_pooled_kernel(const float* h, int64
   }
 }
 
-// Grid (B/PRB row blocks) x (D/64 column blocks). Each block LayerNorms its PRB
-// pooled rows into LDS (layout [i][row]: one ds_read_b128 = 4 rows of element i),
-// then thread (c, part) accumulates column c over a quarter of d for all PRB rows
-// with coalesced projT [d][D] reads; the 4 parts are summed through LDS. The
+// Grid (B/PRB row blocks) x (D/64 column blocks), 16 waves. Each block LayerNorms its PRB
+// pooled rows into LDS (layout [i][row]: one ds_read_b128 = 4 rows of element i), then thread
+// (c, part) accumulates column c over a sixteenth of d for all PRB rows with coalesced projT
+// [d][D] reads; the 16 parts are summed through LDS in part order. (4 parts of d/4 left each
+// thread a 192-long dependent chain of loads and FMAs: ~30 us per launch at B = 256.) The
 // un-normalised rows go to `tmp`; finish_rows_kernel applies the L2 norm.
-constexpr int PRB = 8;
-__global__ __launch_bounds__(256) void pool_project_kernel(const float* h, int64_t ldh, int B, int T, int d,
-                                                           const int32_t* ids, int eos, const float* g,
-                                                           const float* bt, float eps, const float* projT, int D,
-                                                           float* tmp) {
+constexpr int PRB = 8, PP = 16;
+__global__ __launch_bounds__(64 * PP) void pool_project_kernel(const float* h, int64_t ldh, int B, int T, int d,
+                                                               const int32_t* ids, int eos, const float* g,
+                                                               const float* bt, float eps, const float* projT, int D,
+                                                               float* tmp) {
   // Batch invariance: a row's arithmetic must not depend on its slot r in the PRB group.
   // With implicit contraction the compiler fuses (or SLP-packs unfused) the unrolled
   // per-slot chains differently, 1-ulp apart; so no implicit contraction here, and every
@@ -401,10 +402,10 @@ __global__ __launch_bounds__(256) void pool_project_kernel(const float* h, int64
 #pragma clang fp contract(off)
   extern __shared__ __attribute__((aligned(16))) float sm[];
   float* y = sm;                   // [d][PRB]
-  float* part_sum = sm + d * PRB;  // [4][PRB][64]
+  float* part_sum = sm + d * PRB;  // [PP][PRB][64]
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int b0 = blockIdx.x * PRB;
-  for (int rr = wid; rr < PRB; rr += 4) {
+  for (int rr = wid; rr < PRB; rr += PP) {
     const int b = b0 + rr;
     if (b >= B) {
       for (int e = lane; e < d; e += 64) y[e * PRB + rr] = 0.f;
@@ -423,7 +424,7 @@ __global__ __launch_bounds__(256) void pool_project_kernel(const float* h, int64
   __syncthreads();
   const int c = lane, part = wid;
   const int j = blockIdx.y * 64 + c;
-  const int i0 = part * (d / 4), i1 = i0 + d / 4;
+  const int i0 = part * (d / PP), i1 = i0 + d / PP;
   float acc[PRB];
 #pragma unroll
   for (int r = 0; r < PRB; ++r) acc[r] = 0.f;
@@ -441,13 +442,13 @@ __global__ __launch_bounds__(256) void pool_project_kernel(const float* h, int64
 #pragma unroll
   for (int r = 0; r < PRB; ++r) part_sum[(part * PRB + r) * 64 + c] = acc[r];
   __syncthreads();
-  if (part == 0 && j < D) {
+  if (wid < PRB && j < D) {   // wave r sums row r's 16 parts, in part order
+    const int r = wid, b = b0 + r;
+    if (b < B) {
+      float t = part_sum[r * 64 + c];
 #pragma unroll
-    for (int r = 0; r < PRB; ++r) {
-      const int b = b0 + r;
-      if (b >= B) continue;
-      tmp[(int64_t)b * D + j] = part_sum[r * 64 + c] + part_sum[(PRB + r) * 64 + c] +
-                                part_sum[(2 * PRB + r) * 64 + c] + part_sum[(3 * PRB + r) * 64 + c];
+      for (int q = 1; q < PP; ++q) t += part_sum[(q * PRB + r) * 64 + c];
+      tmp[(int64_t)b * D + j] = t;
     }
   }
 }
@@ -658,10 +659,10 @@ hipError_t pool_project(const float* h, int64_t ldh, int B, int T, int d, const 
                         const float* g, const float* bta, float eps, const float* projT, int D, float* tmp, void* out,
                         int out_dtype, int normalize, hipStream_t s) {
   if (B <= 0) return hipSuccess;
-  if (d % 4) return hipErrorInvalidValue;
-  const size_t sm = (size_t)(d * PRB + 4 * PRB * 64) * sizeof(float);
+  if (d % PP) return hipErrorInvalidValue;
+  const size_t sm = (size_t)(d * PRB + PP * PRB * 64) * sizeof(float);
   dim3 grid((B + PRB - 1) / PRB, (D + 63) / 64);
-  pool_project_kernel<<<grid, 256, sm, s>>>(h, ldh, B, T, d, ids, eos, g, bta, eps, projT, D, tmp);
+  pool_project_kernel<<<grid, 64 * PP, sm, s>>>(h, ldh, B, T, d, ids, eos, g, bta, eps, projT, D, tmp);
   finish_rows_kernel<<<(B + 3) / 4, 256, 0, s>>>(tmp, B, D, out, out_dtype, normalize);
   return hipGetLastError();
 }
