@@ -74,6 +74,7 @@ def parse_args(argv=None):
     ap.add_argument("--no-search", action="store_true")
     ap.add_argument("--no-l14", action="store_true", help="skip the ViT-L/14@336 (configs[3]) leg")
     ap.add_argument("--no-parity-mode", action="store_true", help="skip the fp16 parity-mode step")
+    ap.add_argument("--no-varlen", action="store_true", help="skip the mixed-length caption (varlen) leg")
     ap.add_argument("--sequential", action="store_true", help="towers back to back on one stream, no graph")
     ap.add_argument("--split", type=int, default=0, help="sub-batches per tower in encode_pair (0 = library default)")
     return ap.parse_args(argv)
@@ -380,6 +381,37 @@ def pmc_summary():
     return json.load(open(f)), os.path.basename(f)
 
 
+def varlen_leg(model, cfg, dev, B, imgs, steps, warmup, rank=0):
+    """Mixed-length captions (lengths uniform in [8, 77], padded to 77 with EOS as the CLIP
+    tokenizer pads): the library's default varlen text path encodes each caption's live rows only
+    (through its first EOS; causal tower, bit-identical embeddings, tests/test_gpu_encode.py::
+    test_text_varlen_bit_identical) vs every padded row (clm_debug_set bit 32). Not the headline:
+    the headline captions are full 77-token ones, where every row is live."""
+    from clip_lora_match_amd import _capi as C
+    ids = torch.from_numpy(syn.captions(B, cfg.max_pos, cfg.bos_token_id, cfg.eos_token_id, 4242 + rank)).to(dev)
+    live = int(sum(min(int((r == cfg.eos_token_id).nonzero()[0]) + 1, cfg.max_pos) for r in ids.cpu()))
+    oi = torch.empty((B, cfg.proj_dim), dtype=torch.float32, device=dev)
+    ot = torch.empty_like(oi)
+    res = {}
+    try:
+        for name, flag in (("varlen", 0), ("padded", 32)):
+            C.lib().clm_debug_set(flag)
+            for _ in range(warmup):
+                model.encode_pair(imgs, ids, out_img=oi, out_txt=ot, graph=True)
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(steps):
+                model.encode_pair(imgs, ids, out_img=oi, out_txt=ot, graph=True)
+            torch.cuda.synchronize()
+            dt = (time.perf_counter() - t0) / steps
+            res[name] = {"value": round(B / dt, 1), "ms_per_step": round(dt * 1e3, 4)}
+    finally:
+        C.lib().clm_debug_set(0)
+    return {"unit": "image+text pairs/s", "captions": "lengths uniform in [8, 77], padded to 77",
+            "live_text_rows": live, "padded_text_rows": B * cfg.max_pos, **res,
+            "note": "varlen = each caption's rows through its first EOS (the pooled row) only; same embeddings"}
+
+
 def parity_mode_leg(cfg, sd, lora, dev, B, imgs, ids, steps, warmup, lora_mode):
     """The same encode step with fp16 operands: the precision that meets the 1e-3 score bar."""
     m = ClipLoraModel(cfg, device=dev, compute_dtype="float16", lora_mode=lora_mode, max_batch=B)
@@ -431,7 +463,10 @@ def main():
     model.finalize()
 
     imgs = torch.from_numpy(syn.images_u8(B, cfg.image_size, 1234 + rank * B)).to(dev)
-    ids = torch.from_numpy(syn.captions(B, cfg.max_pos, cfg.bos_token_id, cfg.eos_token_id, 99 + rank)).to(dev)
+    # full 77-token captions (every row live): the headline workload is the same with or without
+    # the varlen text path; mixed lengths are the separate `varlen_text` leg
+    ids = torch.from_numpy(syn.captions(B, cfg.max_pos, cfg.bos_token_id, cfg.eos_token_id, 99 + rank,
+                                        min_len=cfg.max_pos)).to(dev)
     emb = torch.empty((2 * B, cfg.proj_dim), dtype=torch.float32, device=dev)
     profiling = [False]
     gathered = torch.empty((world * 2 * B, cfg.proj_dim), dtype=torch.float32, device=dev) if world > 1 else None
@@ -492,7 +527,7 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "bf16" if args.dtype == "bfloat16" else "fp16",
-        "data": "synthetic (seeded uint8 224x224 RGB images, 77-token id captions; deterministic synthetic weights)",
+        "data": "synthetic (seeded uint8 224x224 RGB images, full 77-token id captions; deterministic synthetic weights)",
         "config": {"workload": "ViT-B/32 + LoRA r=8 alpha=16 (q,k,v,out, both towers) encode + L2-normalise",
                    "execution": "sequential" if args.sequential else
                        f"image / text towers concurrently on 2 HIP streams (sub-batches per tower: {args.split or 1})"
@@ -525,6 +560,11 @@ def main():
         result["dist"] = {"backend": backend, "world_size": torch.distributed.get_world_size()}
         if os.environ.get("CLM_REHEARSAL"):
             result["rehearsal"] = os.environ["CLM_REHEARSAL"]
+    if world == 1 and not args.no_varlen:
+        try:
+            result["varlen_text"] = varlen_leg(model, cfg, dev, B, imgs, args.steps, args.warmup, rank)
+        except Exception as e:  # report, never hide
+            result["varlen_text"] = {"error": repr(e)}
     if rank == 0 and world == 1 and not args.no_parity_mode:
         try:
             result["parity_mode"] = parity_mode_leg(cfg, sd, lora, dev, B, imgs, ids, args.steps, args.warmup,

@@ -132,6 +132,9 @@ struct Tower {
   float2* lnst = nullptr;   // [maxM] (rstd, -rstd * mean) of the pending LayerNorm (ln_fold)
   float* hc = nullptr;      // [max_batch, d] pooled residual rows of the pruned last layer
   u16* Oc = nullptr;        // [max_batch, ldo] their attention-output rows
+  // varlen text plan (text_plan): per caption live rows / offsets, packed-row map, fused-attention
+  // tiles, {live rows, tiles}; a sub-batch view at b0 uses lens / tiles + b0, offs / counts + 2 b0
+  int *vl_lens = nullptr, *vl_offs = nullptr, *vl_rowmap = nullptr, *vl_tiles = nullptr, *vl_counts = nullptr;
   int64_t ldx = 0, ldo = 0, ldm = 0;
 };
 
@@ -483,6 +486,13 @@ int build_tower(clm_ctx* c, Tower& T, bool vision) {
   }
   if ((r = c->dalloc(&T.hc, (size_t)B * T.d))) return r;
   if ((r = c->dalloc(&T.Oc, (size_t)B * T.ldo))) return r;
+  if (!T.vision) {
+    if ((r = c->dalloc(&T.vl_lens, (size_t)B))) return r;
+    if ((r = c->dalloc(&T.vl_offs, (size_t)2 * B + 1))) return r;
+    if ((r = c->dalloc(&T.vl_rowmap, (size_t)T.maxM))) return r;
+    if ((r = c->dalloc(&T.vl_tiles, (size_t)B))) return r;
+    if ((r = c->dalloc(&T.vl_counts, (size_t)2 * B))) return r;
+  }
   return CLM_OK;
 }
 
@@ -556,6 +566,21 @@ bool prune_last_layer() {
   return v == 1 && !(g_gemm_debug & 8);   // clm_debug_set bit 8: every row (tests)
 }
 
+// Varlen text (default; $CLM_TEXT_VARLEN=0 or clm_debug_set bit 32: every padded row): the text
+// tower is causal and pools each caption's first-EOS row, so rows after it cannot reach the
+// output. Only each caption's live rows (through its first EOS) are packed and encoded; the
+// embeddings are bit-identical to encoding all L rows (rows are independent in every kernel but
+// attention, whose keys of a live query are all live; tests/test_gpu_encode.py). Needs the fused
+// attention kernel, no LayerNorm folding and no unmerged-LoRA K-extension.
+bool text_varlen_enabled() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("CLM_TEXT_VARLEN");
+    v = (e && !atoi(e)) ? 0 : 1;
+  }
+  return v == 1 && !(g_gemm_debug & 32);
+}
+
 // q/k/v projection + attention fused into one launch for T <= 128 (k_gemm_attn.hip) unless
 // $CLM_FUSED_ATTN=0 or clm_debug_set bit 16 (tests: the two-kernel path, bit-identical)
 bool fused_attention(int T, int H, int d, int K) {
@@ -576,11 +601,22 @@ bool fused_attention(int T, int H, int d, int K) {
 // the LayerNorm kernel and the unfolded fc1 (its pooled rows are computed the same way pruned
 // or not).
 int run_layers(clm_ctx* c, Tower& T, int B, int S, bool causal, const int32_t* ids, bool* pooled_rows,
-               hipStream_t st) {
+               hipStream_t st, bool vl = false) {
   const bool bf = c->bf16();
   const bool prune = prune_last_layer();
   const bool fold = c->ln_fold;
   *pooled_rows = false;
+  // varlen (packed live text rows): the row-wise kernels read the live row count from
+  // T.vl_counts; the profiled pass (no graph, may sync) counts the executed rows and attention pairs
+  const int* mdev = vl ? T.vl_counts : nullptr;
+  double Mx = (double)B * S, attn_pairs = (double)B * S * S;
+  if (vl && c->prof) {
+    std::vector<int> lens(B);
+    HIPCHK(hipMemcpyAsync(lens.data(), T.vl_lens, (size_t)B * 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    Mx = attn_pairs = 0;
+    for (int v : lens) { Mx += v; attn_pairs += (double)v * v; }
+  }
   // residual GEMM that also produces the next LayerNorm's statistics (fold), then finalize them
   auto resid_stats = [&](GemmArgs& g, int64_t M) -> int {
     g.hb = T.X; g.ldhb = T.ldx; g.stats = T.stats;
@@ -619,7 +655,11 @@ int run_layers(clm_ctx* c, Tower& T, int B, int S, bool causal, const int32_t* i
     } else {
       g.W = Lw.w_qkv; g.ldw = Lw.k_qkv; g.bias = Lw.b_qkv;
     }
-    if (!g.lnstat && fused_attention(S, T.H, T.d, g.K)) {
+    if (vl) {   // packed live rows of variable-length captions
+      PROF(CLM_PROF_GEMM, 2.0 * Mx * g.N * g.K + 4.0 * T.H * attn_pairs * 64);
+      KCHK(gemm_attn_varlen(bf, causal, g.A, g.lda, g.W, g.ldw, g.bias, T.O, T.ldo, B, S, T.H, T.d, g.K, T.vl_lens,
+                            T.vl_offs, T.vl_tiles, T.vl_counts, st));
+    } else if (!g.lnstat && fused_attention(S, T.H, T.d, g.K)) {
       // one launch: the q/k/v GEMM's tiles attend their own sequences (GEMM + attention FLOPs)
       PROF(CLM_PROF_GEMM, 2.0 * M * g.N * g.K + 4.0 * B * T.H * (double)S * S * 64);
       KCHK(gemm_attn(bf, causal, g.A, g.lda, g.W, g.ldw, g.bias, T.O, T.ldo, B, S, T.H, T.d, g.K, st));
@@ -633,7 +673,8 @@ int run_layers(clm_ctx* c, Tower& T, int B, int S, bool causal, const int32_t* i
     const bool pooled = prune && last;
     if (pooled) {
       { PROF(CLM_PROF_OTHER, (double)B * T.d * 6.0);
-        KCHK(gather_pooled(T.h, T.d, T.O, T.ldo, B, S, T.d, ids, c->desc.eos_token_id, T.hc, T.Oc, T.ldo, st)); }
+        KCHK(gather_pooled(T.h, T.d, T.O, T.ldo, B, S, T.d, ids, c->desc.eos_token_id, T.hc, T.Oc, T.ldo, st,
+                           vl ? T.vl_offs : nullptr)); }
       M = B;
       h = T.hc;
       O = T.Oc;
@@ -655,10 +696,13 @@ int run_layers(clm_ctx* c, Tower& T, int B, int S, bool causal, const int32_t* i
         int r = pooled_resid(g);
         if (r) return r;
       } else {
-        PROF(CLM_PROF_GEMM, 2.0 * M * g.N * g.K); KCHK(gemm(bf, EPI_RESID, g, st));
+        g.m_dev = mdev;
+        PROF(CLM_PROF_GEMM, 2.0 * Mx * g.N * g.K); KCHK(gemm(bf, EPI_RESID, g, st));
       }
-      PROF(CLM_PROF_LN, (double)M * T.d * 6.0);
-      KCHK(layernorm(bf, ln_into_x(c, T, M, Lw.ln2_g, Lw.ln2_b, Lw.a_fc1, Lw.r_fc1, h), st));
+      LnArgs ln = ln_into_x(c, T, M, Lw.ln2_g, Lw.ln2_b, Lw.a_fc1, Lw.r_fc1, h);
+      if (!pooled) ln.m_dev = mdev;
+      PROF(CLM_PROF_LN, (pooled ? (double)M : Mx) * T.d * 6.0);
+      KCHK(layernorm(bf, ln, st));
     }
     g = GemmArgs{};
     g.A = T.X; g.lda = T.ldx; g.M = (int)M; g.N = T.mlp; g.K = Lw.k_fc1; g.out = T.Hm; g.ldo = T.ldm;
@@ -667,7 +711,8 @@ int run_layers(clm_ctx* c, Tower& T, int B, int S, bool causal, const int32_t* i
     } else {
       g.W = Lw.w_fc1; g.ldw = Lw.k_fc1; g.bias = Lw.b_fc1;
     }
-    { PROF(CLM_PROF_GEMM, 2.0 * M * g.N * g.K);   // pooled rows: 64 x 128 tiles (config 5) fill the chip
+    if (!pooled) g.m_dev = mdev;
+    { PROF(CLM_PROF_GEMM, 2.0 * (pooled ? (double)M : Mx) * g.N * g.K);   // pooled rows: 64 x 128 tiles (config 5) fill the chip
       KCHK(pooled && pooled_small ? gemm_cfg(bf, EPI_GELU, 5, g, st) : gemm(bf, g.lnstat ? EPI_GELU_LN : EPI_GELU, g, st)); }
     if (Lw.r_fc2) { PROF(CLM_PROF_OTHER, 2.0 * M * T.mlp + 4.0 * Lw.r_fc2 * T.mlp);
       KCHK(lora_down(bf, T.Hm, T.ldm, (int)M, T.mlp, Lw.a_fc2, Lw.r_fc2, RPAD, st)); }
@@ -682,12 +727,15 @@ int run_layers(clm_ctx* c, Tower& T, int B, int S, bool causal, const int32_t* i
         int r = pooled_resid(g);
         if (r) return r;
       } else {
-        PROF(CLM_PROF_GEMM, 2.0 * M * g.N * g.K); KCHK(gemm(bf, EPI_RESID, g, st));
+        g.m_dev = mdev;
+        PROF(CLM_PROF_GEMM, 2.0 * Mx * g.N * g.K); KCHK(gemm(bf, EPI_RESID, g, st));
       }
       if (!last) {
         LayerW& Ln = T.layers[l + 1];
-        PROF(CLM_PROF_LN, (double)M * T.d * 6.0);
-        KCHK(layernorm(bf, ln_into_x(c, T, M, Ln.ln1_g, Ln.ln1_b, Ln.a_qkv, Ln.r_qkv), st));
+        LnArgs ln = ln_into_x(c, T, M, Ln.ln1_g, Ln.ln1_b, Ln.a_qkv, Ln.r_qkv);
+        ln.m_dev = mdev;
+        PROF(CLM_PROF_LN, Mx * T.d * 6.0);
+        KCHK(layernorm(bf, ln, st));
       }
     }
   }
@@ -705,6 +753,9 @@ Tower ws_view(const Tower& T0, int b0, int rows, int patches, int proj_dim) {
   T.Oc += (int64_t)b0 * T.ldo;
   if (T.stats) T.stats += r0 * (T.d / 32);
   if (T.lnst) T.lnst += r0;
+  if (T.vl_lens) {
+    T.vl_lens += b0; T.vl_tiles += b0; T.vl_offs += 2 * b0; T.vl_counts += 2 * b0; T.vl_rowmap += r0;
+  }
   return T;
 }
 
@@ -741,14 +792,24 @@ int encode_text_chunk(clm_ctx* c, Tower& T, const int32_t* ids_dev, int B, int L
   a.hf = T.h; a.ldh = T.d; a.g1 = T.layers[0].ln1_g; a.b1 = T.layers[0].ln1_b;
   a.y = T.X; a.ldy = T.ldx; a.loraA = T.layers[0].a_qkv; a.r_ext = T.layers[0].r_qkv;
   a.r_pad = a.loraA ? RPAD : 0; a.M = B * L; a.d = T.d; a.eps = d.ln_eps;
+  bool vl = text_varlen_enabled() && T.vl_lens && !c->ln_fold && B <= 4096 &&   // text_plan: <= 4096 captions per chunk
+            fused_attention(L, T.H, T.d, T.layers.empty() ? 0 : T.layers[0].k_qkv);
+  for (const LayerW& Lw : T.layers) vl = vl && !Lw.r_qkv && !Lw.r_out && !Lw.r_fc1 && !Lw.r_fc2;
+  if (vl) {
+    { PROF(CLM_PROF_OTHER, (double)B * L * 8.0);
+      KCHK(text_plan(ids_dev, B, L, d.eos_token_id, T.vl_lens, T.vl_offs, T.vl_rowmap, T.vl_tiles, T.vl_counts, st)); }
+    a.m_dev = T.vl_counts;
+    a.rowmap = T.vl_rowmap;
+  }
   { PROF(CLM_PROF_LN, (double)B * L * T.d * 14.0); KCHK(layernorm(bf, a, st)); }
   bool pooled_rows = false;
-  int r = run_layers(c, T, B, L, true, ids_dev, &pooled_rows, st);
+  int r = run_layers(c, T, B, L, true, ids_dev, &pooled_rows, st, vl);
   if (r) return r;
   { PROF(CLM_PROF_OTHER, (double)B * (T.d * 4.0 + d.proj_dim * 4.0 + L * 4.0) + (double)T.d * d.proj_dim * 4.0);
     KCHK(pool_project(pooled_rows ? T.hc : T.h, T.d, B, pooled_rows ? 1 : L, T.d, pooled_rows ? nullptr : ids_dev,
                       d.eos_token_id, T.fin_g, T.fin_b, d.ln_eps, T.projT,
-                      d.proj_dim, T.pooled, out, out_dtype == CLM_F32 ? 0 : 1, normalize, st)); }
+                      d.proj_dim, T.pooled, out, out_dtype == CLM_F32 ? 0 : 1, normalize, st,
+                      vl && !pooled_rows ? T.vl_offs : nullptr)); }
   return CLM_OK;
 }
 
@@ -1112,7 +1173,9 @@ int clm_encode_pair(clm_ctx* ctx, const void* pixels, int pix_layout, int n_img,
                         out_dtype, normalize);
     if (r) return r;
   } else {
-    clm_ctx::PairKey key(pixels, pix_layout, n_img, ids, n_txt, L, out_img, out_txt, out_dtype, normalize, split);
+    // the diagnostic flags change which kernels run (varlen / fused / pruned): part of the key
+    clm_ctx::PairKey key(pixels, pix_layout, n_img, ids, n_txt, L, out_img, out_txt, out_dtype, normalize,
+                         split | (g_gemm_debug << 8));
     auto it = ctx->graphs.find(key);
     if (it == ctx->graphs.end()) {
       if (ctx->graphs.size() >= 16) ctx->drop_graphs();

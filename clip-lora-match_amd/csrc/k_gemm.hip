@@ -35,8 +35,10 @@ using namespace gemm_detail;
 // runs, and the epilogue's stores drain under tile i+1's main loop (counted vmcnt that
 // leaves them in flight). A one-tile-per-workgroup grid is the plain non-persistent GEMM.
 template <bool BF, int EPI, int BM, int BN, int WM, int WN, int STAGES>
-__global__ __launch_bounds__(WM * WN * 64, (Cfg<BM, BN, WM, WN, STAGES>::WAVES_PER_EU)) void gemm_kernel(GemmArgs g) {
+__global__ __launch_bounds__(WM * WN * 64, (Cfg<BM, BN, WM, WN, STAGES>::WAVES_PER_EU)) void gemm_kernel(GemmArgs ga) {
   using C = Cfg<BM, BN, WM, WN, STAGES>;
+  GemmArgs g = ga;   // varlen: the device-resident row count (the grid was sized for ga.M)
+  if (g.m_dev) g.M = __builtin_amdgcn_readfirstlane(*g.m_dev);
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -44,6 +46,7 @@ __global__ __launch_bounds__(WM * WN * 64, (Cfg<BM, BN, WM, WN, STAGES>::WAVES_P
   const int ks = g.ksplit > 1 ? g.ksplit : 1;   // split-K: work unit = (tile, K slice)
   const int ntiles = ntn * ntm * ks, G = gridDim.x;
   const int xb = xcd_remap(blockIdx.x, G);
+  if (xb >= ntiles) return;   // varlen: fewer live tiles than the grid
   const int n_my = (ntiles - 1 - xb) / G + 1;
   const int nk = g.K / BK / ks;
   const int S = n_my * nk;   // K-steps of all this workgroup's tiles, one ring

@@ -35,8 +35,10 @@ struct Cfg2 {
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
 
 template <bool BF, int EPI, int BM, int BN, int WM, int WN, bool DEFER, int NS>
-__global__ __launch_bounds__(WM * WN * 64, 1) void gemm2_kernel(GemmArgs g) {
+__global__ __launch_bounds__(WM * WN * 64, 1) void gemm2_kernel(GemmArgs ga) {
   using C = Cfg2<BM, BN, WM, WN, NS>;
+  GemmArgs g = ga;   // varlen: the device-resident row count (the grid was sized for ga.M)
+  if (g.m_dev) g.M = __builtin_amdgcn_readfirstlane(*g.m_dev);
   static_assert(NS == 2 || NS == 3, "ring of 2 or 3 buffers");
   constexpr int L = C::LA + C::LB;   // vmcnt units (DMA instructions) per K-step
   constexpr int TM = C::TM, TN = C::TN;
@@ -47,6 +49,7 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void gemm2_kernel(GemmArgs g) {
   const int ntn = (g.N + BN - 1) / BN, ntm = (g.M + BM - 1) / BM;
   const int ntiles = ntn * ntm, G = gridDim.x;
   const int xb = xcd_remap(blockIdx.x, G);
+  if (xb >= ntiles) return;   // varlen: fewer live tiles than the grid
   const int n_my = (ntiles - 1 - xb) / G + 1;
   const int nk = g.K / BK;
   const int S = n_my * nk;

@@ -226,6 +226,7 @@ hipError_t by_epi3(int epi, const GemmArgs& g, hipStream_t s) {
 }  // namespace
 
 hipError_t gemm3_launch(bool bf16, int epi, const GemmArgs& g, hipStream_t s) {
+  if (g.m_dev) return hipErrorInvalidValue;   // varlen rows: gemm_kernel / G2 only
   if (g.M > 0 && (int64_t)g.lda * 2 * 256 > 0x7FFFFFF0LL) return hipErrorInvalidValue;   // descriptor range
   return bf16 ? by_epi3<true>(epi, g, s) : by_epi3<false>(epi, g, s);
 }

@@ -17,6 +17,8 @@
 // per wave), 2-stage global_load_lds ring, swapped MFMA operands (so the accumulator
 // MFMA order, hence every q/k/v value, equals the qkv GEMM's). One tile per workgroup: the
 // 96 KB staging image reuses the ring's LDS.
+#include <algorithm>
+
 #include "gemm_common.hpp"
 
 namespace clm {
@@ -55,19 +57,36 @@ struct FaArgs {
   const float* bias;           // [3d]
   u16* out; int64_t ldo;       // [B*T, >= d] attention output
   int B, T, H, d, K, G;        // G = sequences per tile
+  // varlen (VL): packed sequences of lens[b] rows at offs[b]; tiles[t] = first | count << 16;
+  // counts = {live rows, live tiles}
+  const int* lens; const int* offs; const int* tiles; const int* counts;
 };
 
-template <bool BF, bool CAUSAL>
+template <bool BF, bool CAUSAL, bool VL>
 __global__ __launch_bounds__(FA_NW * 64, 2) void gemm_attn_kernel(FaArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   // the H head tiles of one row panel run back to back on one XCD (they share the A panel in L2)
-  const int t = xcd_remap(blockIdx.x, gridDim.x);
-  const int tm = t / a.H, h = t - tm * a.H;
-  const int s0 = tm * a.G;                // first sequence of the tile
-  const int64_t m0 = (int64_t)s0 * a.T;   // its first row
-  const int64_t M = (int64_t)a.B * a.T;
+  int t, s0, nseq;
+  int64_t m0, M;
+  if constexpr (VL) {   // grid sized for the worst case: only the live tiles run
+    const int live = __builtin_amdgcn_readfirstlane(a.counts[1]) * a.H;
+    if ((int)blockIdx.x >= live) return;
+    t = xcd_remap(blockIdx.x, live);
+    const int tw = __builtin_amdgcn_readfirstlane(a.tiles[t / a.H]);
+    s0 = tw & 0xFFFF;
+    nseq = tw >> 16;
+    m0 = __builtin_amdgcn_readfirstlane(a.offs[s0]);
+    M = __builtin_amdgcn_readfirstlane(a.counts[0]);
+  } else {
+    t = xcd_remap(blockIdx.x, gridDim.x);
+    s0 = (t / a.H) * a.G;
+    nseq = min(a.G, a.B - s0);
+    m0 = (int64_t)s0 * a.T;
+    M = (int64_t)a.B * a.T;
+  }
+  const int h = t % a.H;
   const int nk = a.K / BK;
 
   // ---- main loop: acc[256 x 192] = X[m0 .. m0 + 255, :] . W[head h's q, k, v rows]^T --------
@@ -161,12 +180,26 @@ __global__ __launch_bounds__(FA_NW * 64, 2) void gemm_attn_kernel(FaArgs a) {
   const uint8_t* sQ = smem;
   const uint8_t* sK = smem + FA_SEC;
   const uint8_t* sV = smem + 2 * FA_SEC;
-  const int T = a.T;
-  const int nseq = min(a.G, a.B - s0);
-  const int nqb = (T + 15) / 16, ntiles = (T + 63) / 64;
-  for (int u = wid; u < nseq * nqb; u += FA_NW) {
-    const int i = u / nqb, q0 = (u - i * nqb) * 16;
-    const int r0 = i * T;                  // the sequence's first tile row
+  // units (sequence i, 16-query block) in order, unit u to wave u % 8
+  int u = 0, i = 0, qb = 0, nqb = 0, seq_t = 0, seq_r0 = 0;
+  auto load_seq = [&]() {   // sequence i: its length and first tile row
+    if constexpr (VL) {
+      seq_t = a.lens[s0 + i];
+      seq_r0 = a.offs[s0 + i] - (int)m0;
+    } else {
+      seq_t = a.T;
+      seq_r0 = i * a.T;
+    }
+    nqb = (seq_t + 15) / 16;
+    qb = 0;
+  };
+  if (nseq > 0) load_seq();
+  for (; i < nseq; ++u) {
+    const int q0 = qb * 16, T = seq_t, r0 = seq_r0;
+    const bool mine = (u % FA_NW) == wid;
+    if (++qb == nqb && ++i < nseq) load_seq();
+    if (!mine) continue;
+    const int ntiles = (T + 63) / 64;
     const int qi = q0 + (lane & 15);       // this lane's query
     u32x4 qa[2];
     {
@@ -230,7 +263,7 @@ __global__ __launch_bounds__(FA_NW * 64, 2) void gemm_attn_kernel(FaArgs a) {
     rs = cross_rows_reduce<false>(rs);
     if (qi < T) {
       const float inv = 1.0f / rs;
-      u16* op = a.out + (m0 + r0 + qi) * a.ldo + h * 64 + 4 * g;
+      u16* op = a.out + (m0 + r0 + qi) * a.ldo + h * 64 + 4 * g;   // row of sequence i, query qi
 #pragma unroll
       for (int nb = 0; nb < 4; ++nb)
         *(u32x2*)(op + nb * 16) = u32x2{pack2<BF>(o[nb][0] * inv, o[nb][1] * inv), pack2<BF>(o[nb][2] * inv, o[nb][3] * inv)};
@@ -238,9 +271,9 @@ __global__ __launch_bounds__(FA_NW * 64, 2) void gemm_attn_kernel(FaArgs a) {
   }
 }
 
-template <bool BF, bool CAUSAL>
+template <bool BF, bool CAUSAL, bool VL>
 hipError_t launch(const FaArgs& a, int tiles, hipStream_t s) {
-  auto kern = gemm_attn_kernel<BF, CAUSAL>;
+  auto kern = gemm_attn_kernel<BF, CAUSAL, VL>;
   static unsigned dev_done = 0;   // >64 KiB dynamic LDS needs the opt-in attribute, once per device
   int dev = 0;
   (void)hipGetDevice(&dev);
@@ -268,8 +301,28 @@ hipError_t gemm_attn(bool bf16, bool causal, const u16* X, int64_t ldx, const u1
   a.B = B; a.T = T; a.H = H; a.d = d; a.K = K; a.G = FA_BM / T;
   const int64_t tiles = (int64_t)((B + a.G - 1) / a.G) * H;
   if (tiles > 0x7FFFFFFF) return hipErrorInvalidValue;
-  if (bf16) return causal ? launch<true, true>(a, (int)tiles, s) : launch<true, false>(a, (int)tiles, s);
-  return causal ? launch<false, true>(a, (int)tiles, s) : launch<false, false>(a, (int)tiles, s);
+  if (bf16) return causal ? launch<true, true, false>(a, (int)tiles, s) : launch<true, false, false>(a, (int)tiles, s);
+  return causal ? launch<false, true, false>(a, (int)tiles, s) : launch<false, false, false>(a, (int)tiles, s);
+}
+
+hipError_t gemm_attn_varlen(bool bf16, bool causal, const u16* X, int64_t ldx, const u16* W, int64_t ldw,
+                            const float* bias, u16* out, int64_t ldo, int B, int L, int H, int d, int K,
+                            const int* lens, const int* offs, const int* tiles, const int* counts, hipStream_t s) {
+  if (B <= 0) return hipSuccess;
+  if (!gemm_attn_supported(L, H, d, K) || B > 0xFFFF || (ldx % 8) || (ldw % 8) || (ldo % 4) || ldx < K || ldw < K ||
+      ldo < d || !lens || !offs || !tiles || !counts)
+    return hipErrorInvalidValue;
+  FaArgs a{};
+  a.X = X; a.ldx = ldx; a.W = W; a.ldw = ldw; a.bias = bias; a.out = out; a.ldo = ldo;
+  a.B = B; a.T = L; a.H = H; a.d = d; a.K = K; a.G = 0;
+  a.lens = lens; a.offs = offs; a.tiles = tiles; a.counts = counts;
+  // text_plan closes a tile only when the next sequence does not fit, so every tile but the last
+  // holds more than 256 - L rows: at most ceil(rows / (257 - L)) + 1 tiles, and at most B
+  const int64_t max_tiles = std::min<int64_t>(B, ((int64_t)B * L + (256 - L)) / (257 - L) + 1);
+  const int64_t grid = max_tiles * H;
+  if (grid > 0x7FFFFFFF) return hipErrorInvalidValue;
+  if (bf16) return causal ? launch<true, true, true>(a, (int)grid, s) : launch<true, false, true>(a, (int)grid, s);
+  return causal ? launch<false, true, true>(a, (int)grid, s) : launch<false, false, true>(a, (int)grid, s);
 }
 
 }  // namespace clm

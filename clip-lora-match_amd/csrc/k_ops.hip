@@ -20,7 +20,9 @@ namespace {
 // ------------------------------------------------------------------ LN ------
 // One wave per row; lane owns NP float2 pairs at e = (i*64 + lane)*2.
 template <bool BF, int NP>
-__global__ __launch_bounds__(256) void ln_kernel(LnArgs a) {
+__global__ __launch_bounds__(256) void ln_kernel(LnArgs aa) {
+  LnArgs a = aa;   // varlen: the device-resident row count (the grid was sized for aa.M)
+  if (a.m_dev) a.M = __builtin_amdgcn_readfirstlane(*a.m_dev);
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= a.M) return;
@@ -34,9 +36,10 @@ __global__ __launch_bounds__(256) void ln_kernel(LnArgs a) {
       x[i][0] = v.x; x[i][1] = v.y;
     }
   } else {
-    const int tokid = a.ids[row];
+    const int src = a.rowmap ? a.rowmap[row] : row;   // packed row -> b * L + position
+    const int tokid = a.ids[src];
     const float* tk = a.tok + (int64_t)tokid * d;
-    const float* ps = a.pos + (int64_t)(row % a.L) * d;
+    const float* ps = a.pos + (int64_t)(src % a.L) * d;
 #pragma unroll
     for (int i = 0; i < NP; ++i) {
       const int e = (i * 64 + lane) * 2;
@@ -103,7 +106,9 @@ __global__ __launch_bounds__(256) void ln_kernel(LnArgs a) {
 // d % 256 == 0: lane owns NQ float4 at e = (i*64 + lane)*4 (16-B loads, 8-B bf16 stores: half
 // the memory instructions of the float2 form above; HBM-bound).
 template <bool BF, int NQ>
-__global__ __launch_bounds__(256) void ln4_kernel(LnArgs a) {
+__global__ __launch_bounds__(256) void ln4_kernel(LnArgs aa) {
+  LnArgs a = aa;   // varlen: the device-resident row count (the grid was sized for aa.M)
+  if (a.m_dev) a.M = __builtin_amdgcn_readfirstlane(*a.m_dev);
   // R rows per wave (both rows' loads issued before either is reduced; gamma / beta loaded
   // once per wave and reused)
   constexpr int R = 2;
@@ -120,9 +125,10 @@ __global__ __launch_bounds__(256) void ln4_kernel(LnArgs a) {
 #pragma unroll
       for (int i = 0; i < NQ; ++i) x[r][i] = *(const float4*)(src + (i * 64 + lane) * 4);
     } else {
-      const int tokid = a.ids[row];
+      const int src = a.rowmap ? a.rowmap[row] : row;   // packed row -> b * L + position
+      const int tokid = a.ids[src];
       const float* tk = a.tok + (int64_t)tokid * d;
-      const float* ps = a.pos + (int64_t)(row % a.L) * d;
+      const float* ps = a.pos + (int64_t)(src % a.L) * d;
 #pragma unroll
       for (int i = 0; i < NQ; ++i) {
         const int e = (i * 64 + lane) * 4;
@@ -375,9 +381,9 @@ __device__ __forceinline__ int pooled_row(const int32_t* ids, int b, int T, int 
 // the attention output O into the compact hc [B][d] / Oc [B][ldoc] (see run_layers).
 __global__ __launch_bounds__(64) void gather_pooled_kernel(const float* h, int64_t ldh, const u16* O, int64_t ldo,
                                                            int T, int d, const int32_t* ids, int eos, float* hc,
-                                                           u16* Oc, int64_t ldoc) {
+                                                           u16* Oc, int64_t ldoc, const int* offs) {
   const int b = blockIdx.x, lane = threadIdx.x;
-  const int64_t row = (int64_t)b * T + pooled_row(ids, b, T, eos, lane);
+  const int64_t row = offs ? (int64_t)offs[b + 1] - 1 : (int64_t)b * T + pooled_row(ids, b, T, eos, lane);
   for (int e = lane * 4; e < d; e += 256) {
     *(float4*)(hc + (int64_t)b * d + e) = *(const float4*)(h + row * ldh + e);
     *(u32x2*)(Oc + (int64_t)b * ldoc + e) = *(const u32x2*)(O + row * ldo + e);
@@ -394,7 +400,7 @@ constexpr int PRB = 8, PP = 16;
 __global__ __launch_bounds__(64 * PP) void pool_project_kernel(const float* h, int64_t ldh, int B, int T, int d,
                                                                const int32_t* ids, int eos, const float* g,
                                                                const float* bt, float eps, const float* projT, int D,
-                                                               float* tmp) {
+                                                               float* tmp, const int* offs) {
   // Batch invariance: a row's arithmetic must not depend on its slot r in the PRB group.
   // With implicit contraction the compiler fuses (or SLP-packs unfused) the unrolled
   // per-slot chains differently, 1-ulp apart; so no implicit contraction here, and every
@@ -411,8 +417,8 @@ __global__ __launch_bounds__(64 * PP) void pool_project_kernel(const float* h, i
       for (int e = lane; e < d; e += 64) y[e * PRB + rr] = 0.f;
       continue;
     }
-    const int prow = pooled_row(ids, b, T, eos, lane);
-    const float* x = h + ((int64_t)b * T + prow) * ldh;
+    const int64_t prow = offs ? (int64_t)offs[b + 1] - 1 : (int64_t)b * T + pooled_row(ids, b, T, eos, lane);
+    const float* x = h + prow * ldh;
     float s = 0.f;
     for (int e = lane; e < d; e += 64) s += x[e];
     const float mean = wave_sum(s) / d;
@@ -450,6 +456,78 @@ __global__ __launch_bounds__(64 * PP) void pool_project_kernel(const float* h, i
       for (int q = 1; q < PP; ++q) t += part_sum[(q * PRB + r) * 64 + c];
       tmp[(int64_t)b * D + j] = t;
     }
+  }
+}
+
+// Varlen text plan: live rows per caption (its pooled row + 1: with the causal mask no later row
+// reaches the pooled one), their prefix sums, the packed-row -> [B, L] map and the fused-attention
+// tiles (greedy: whole captions in order, <= 256 rows per tile).
+// live rows per caption, one wave per caption (pooled_row's rule): its own launch, so the id
+// reads of all captions are in flight at once
+__global__ __launch_bounds__(256) void text_lens_kernel(const int32_t* ids, int B, int L, int eos, int* lens) {
+  const int b = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (b >= B) return;
+  const int p = pooled_row(ids, b, L, eos, threadIdx.x & 63);
+  if ((threadIdx.x & 63) == 0) lens[b] = p + 1;
+}
+
+// One workgroup, everything parallel but the walk over tiles: block prefix sum of the lengths in
+// LDS, then per caption b (a thread each) the end of a tile that would start at b (binary search
+// in the prefix sums), then thread 0 chains the tiles from caption 0 (one LDS read per tile).
+// (A sequential per-caption pass in one wave cost 40-110 us at B = 256.)
+constexpr int PLAN_MAX_B = 4096;
+__global__ __launch_bounds__(256) void text_plan_kernel(int B, int L, const int* lens, int* offs, int* rowmap,
+                                                        int* tiles, int* counts) {
+  __shared__ int s_off[PLAN_MAX_B + 1];
+  __shared__ int s_next[PLAN_MAX_B];
+  __shared__ int s_part[256];
+  const int tid = threadIdx.x;
+  const int C = (B + 255) / 256;   // captions per thread, contiguous
+  const int b0 = min(tid * C, B), b1 = min(b0 + C, B);
+  int sum = 0;
+  for (int b = b0; b < b1; ++b) { s_off[b] = sum; sum += lens[b]; }
+  s_part[tid] = sum;
+  __syncthreads();
+  if (tid < 64) {   // exclusive scan of the 256 chunk sums: 4 per lane, then a wave scan
+    const int v0 = s_part[tid * 4], v1 = s_part[tid * 4 + 1], v2 = s_part[tid * 4 + 2], v3 = s_part[tid * 4 + 3];
+    const int own = v0 + v1 + v2 + v3;
+    int t = own;
+    for (int o = 1; o < 64; o <<= 1) {
+      const int y = __shfl_up(t, o, 64);
+      if (tid >= o) t += y;
+    }
+    const int ex = t - own;
+    s_part[tid * 4] = ex;
+    s_part[tid * 4 + 1] = ex + v0;
+    s_part[tid * 4 + 2] = ex + v0 + v1;
+    s_part[tid * 4 + 3] = ex + v0 + v1 + v2;
+    if (tid == 63) {
+      s_off[B] = t;
+      counts[0] = t;
+    }
+  }
+  __syncthreads();
+  for (int b = b0; b < b1; ++b) s_off[b] += s_part[tid];
+  __syncthreads();
+  for (int b = tid; b < B; b += 256) {   // largest e with s_off[e] - s_off[b] <= 256
+    int lo = b + 1, hi = B;
+    const int lim = s_off[b] + 256;
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (s_off[mid] <= lim) lo = mid; else hi = mid - 1;
+    }
+    s_next[b] = lo;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    int nt = 0;
+    for (int first = 0; first < B; first = s_next[first]) tiles[nt++] = first | ((s_next[first] - first) << 16);
+    counts[1] = nt;
+  }
+  for (int b = tid; b <= B; b += 256) offs[b] = s_off[b];
+  for (int b = tid; b < B; b += 256) {
+    const int o = s_off[b], n = s_off[b + 1] - o;
+    for (int p = 0; p < n; ++p) rowmap[o + p] = b * L + p;
   }
 }
 
@@ -648,22 +726,33 @@ hipError_t write_cls(float* h, int64_t ldh, int B, int T, int d, const float* cl
 }
 
 hipError_t gather_pooled(const float* h, int64_t ldh, const u16* O, int64_t ldo, int B, int T, int d,
-                         const int32_t* ids, int eos, float* hc, u16* Oc, int64_t ldoc, hipStream_t s) {
+                         const int32_t* ids, int eos, float* hc, u16* Oc, int64_t ldoc, hipStream_t s,
+                         const int* offs) {
   if (B <= 0) return hipSuccess;
   if ((d % 4) || (ldh % 4) || (ldo % 4) || (ldoc % 4)) return hipErrorInvalidValue;
-  gather_pooled_kernel<<<B, 64, 0, s>>>(h, ldh, O, ldo, T, d, ids, eos, hc, Oc, ldoc);
+  gather_pooled_kernel<<<B, 64, 0, s>>>(h, ldh, O, ldo, T, d, ids, eos, hc, Oc, ldoc, offs);
   return hipGetLastError();
 }
 
 hipError_t pool_project(const float* h, int64_t ldh, int B, int T, int d, const int32_t* ids, int eos,
                         const float* g, const float* bta, float eps, const float* projT, int D, float* tmp, void* out,
-                        int out_dtype, int normalize, hipStream_t s) {
+                        int out_dtype, int normalize, hipStream_t s, const int* offs) {
   if (B <= 0) return hipSuccess;
   if (d % PP) return hipErrorInvalidValue;
   const size_t sm = (size_t)(d * PRB + PP * PRB * 64) * sizeof(float);
   dim3 grid((B + PRB - 1) / PRB, (D + 63) / 64);
-  pool_project_kernel<<<grid, 64 * PP, sm, s>>>(h, ldh, B, T, d, ids, eos, g, bta, eps, projT, D, tmp);
+  pool_project_kernel<<<grid, 64 * PP, sm, s>>>(h, ldh, B, T, d, ids, eos, g, bta, eps, projT, D, tmp, offs);
   finish_rows_kernel<<<(B + 3) / 4, 256, 0, s>>>(tmp, B, D, out, out_dtype, normalize);
+  return hipGetLastError();
+}
+
+hipError_t text_plan(const int32_t* ids, int B, int L, int eos, int* lens, int* offs, int* rowmap, int* tiles,
+                     int* counts, hipStream_t s) {
+  if (B <= 0) return hipSuccess;
+  if (L < 1 || L > 256) return hipErrorInvalidValue;
+  if (B > PLAN_MAX_B) return hipErrorInvalidValue;
+  text_lens_kernel<<<(B + 3) / 4, 256, 0, s>>>(ids, B, L, eos, lens);
+  text_plan_kernel<<<1, 256, 0, s>>>(B, L, lens, offs, rowmap, tiles, counts);
   return hipGetLastError();
 }
 

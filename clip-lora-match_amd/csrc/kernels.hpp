@@ -47,6 +47,9 @@ struct GemmArgs {
   // split-K (gemm_kernel configs only, EPI_SCORE as the fp32 partial store): ksplit > 1 cuts K
   // into ksplit equal slices; slice s of every tile writes out + s * split_stride
   int ksplit; int64_t split_stride;
+  // varlen rows (packed text tower): if set, the row count is *m_dev (device-resident, <= M, which
+  // sizes the grid), so a captured graph replays with data-dependent row counts
+  const int* m_dev;
   int debug;       // diagnostics only: 1 = skip the epilogue (accumulators kept live), 2 = drop its
                    // stores, 4 = one tile per workgroup (non-persistent grid)
 };
@@ -85,6 +88,9 @@ struct LnArgs {
   u16* y; int64_t ldy;
   const float* loraA; int r_ext; int r_pad;   // [r_ext, d] fp32
   int M, d; float eps;
+  // varlen rows (packed text tower): rows r < *m_dev only (M sizes the grid); mode 1 reads token
+  // rowmap[r] = b * L + position of the padded [B, L] ids instead of r
+  const int* m_dev; const int* rowmap;
 };
 hipError_t layernorm(bool bf16, const LnArgs& a, hipStream_t s);
 // per-row LayerNorm statistics from a stats-producing GEMM's 32-column moments (Chan's parallel
@@ -110,11 +116,23 @@ hipError_t write_cls(float* h, int64_t ldh, int B, int T, int d, const float* cl
 //   tmp: [B, D] fp32 workspace
 // Last-layer pruning: hc[b] = h[b*T + prow_b], Oc[b][:d] = O[b*T + prow_b][:d], prow_b the
 // pooled row (0, or the first EOS of ids).
+// offs (varlen packed text rows, see text_plan): item b's pooled row is offs[b + 1] - 1 (its last
+// live row, the first EOS) instead of b * T + pooled_row(ids)
 hipError_t gather_pooled(const float* h, int64_t ldh, const u16* O, int64_t ldo, int B, int T, int d,
-                         const int32_t* ids, int eos, float* hc, u16* Oc, int64_t ldoc, hipStream_t s);
+                         const int32_t* ids, int eos, float* hc, u16* Oc, int64_t ldoc, hipStream_t s,
+                         const int* offs = nullptr);
 hipError_t pool_project(const float* h, int64_t ldh, int B, int T, int d, const int32_t* ids,
                         int eos, const float* g, const float* bta, float eps, const float* projT,
-                        int D, float* tmp, void* out, int out_dtype, int normalize, hipStream_t s);
+                        int D, float* tmp, void* out, int out_dtype, int normalize, hipStream_t s,
+                        const int* offs = nullptr);
+// Varlen text plan (causal text tower, CLIPTextTransformer pools the first EOS row: rows after it
+// cannot reach the pooled output). Per caption b of ids [B, L]: lens[b] = pooled row + 1 live
+// rows, offs[b] = their exclusive prefix sum (offs[B] = total), rowmap[offs[b] + p] = b * L + p,
+// the fused-attention tiles (whole captions, <= 256 rows each; tiles[t] = first caption |
+// captions << 16) and counts = {live rows, tiles}. Two launches (lengths: a wave per caption;
+// prefix / packing / row map: one workgroup); B <= 4096.
+hipError_t text_plan(const int32_t* ids, int B, int L, int eos, int* lens, int* offs, int* rowmap, int* tiles,
+                     int* counts, hipStream_t s);
 
 // ----------------------------------------------------------- attention -----
 // qkv [B*T, 3d] (q pre-scaled by head_dim^-0.5), out [B*T, ldo] compute dtype.
@@ -125,6 +143,11 @@ hipError_t attention(bool bf16, bool causal, const u16* qkv, int64_t ldq, u16* o
 bool gemm_attn_supported(int T, int H, int d, int K);
 hipError_t gemm_attn(bool bf16, bool causal, const u16* X, int64_t ldx, const u16* W, int64_t ldw, const float* bias,
                      u16* out, int64_t ldo, int B, int T, int H, int d, int K, hipStream_t s);
+// the same over packed variable-length sequences (text_plan's lens / offs / tiles / counts; B
+// sequences of <= L <= 128 rows, rows X[offs[b] ..]); grid sized for the worst case
+hipError_t gemm_attn_varlen(bool bf16, bool causal, const u16* X, int64_t ldx, const u16* W, int64_t ldw,
+                            const float* bias, u16* out, int64_t ldo, int B, int L, int H, int d, int K,
+                            const int* lens, const int* offs, const int* tiles, const int* counts, hipStream_t s);
 
 // ----------------------------------------------------------- search --------
 // rows f32|f16 [n, dim] -> fp16 dst + fp32 inverse norms of the fp16-rounded rows

@@ -272,3 +272,44 @@ def test_fused_qkv_attention_bit_identical(preset, dtype, mode):
         C.lib().clm_debug_set(0)
     for i, (a, b) in enumerate(zip(outs[0], outs[16])):
         assert torch.equal(a, b), f"case {i}: fused vs two-kernel max diff {(a - b).abs().max().item():.3e}"
+
+
+@pytest.mark.parametrize("preset,dtype", [("tiny", "float16"), ("ViT-B/32", "bfloat16"), ("ViT-B/32", "float16")])
+def test_text_varlen_bit_identical(preset, dtype):
+    """Varlen text (default): only each caption's live rows -- through its first EOS, the pooled
+    row; the tower is causal, so no later row reaches it -- are packed and encoded (text_plan +
+    gemm_attn_varlen + row-count-from-device GEMMs / LayerNorms). The embeddings must equal the
+    padded every-row encode (clm_debug_set bit 32) bit for bit: ragged lengths, a caption without
+    EOS (pools row 0: one live row), captions filling all L rows, pruned and every-row last layer
+    (bit 8), and the two-stream / graph-replayed pair encode with sub-batches."""
+    from clip_lora_match_amd import _capi as C
+    m, cfg, sd, lora = _model(preset, dtype, max_batch=64)
+    ids = syn.captions(61, cfg.max_pos, cfg.bos_token_id, cfg.eos_token_id, 77, min_len=2)
+    ids[3] = np.arange(cfg.max_pos) + 5           # no EOS at all
+    ids[4, :] = 7
+    ids[4, 0] = cfg.bos_token_id
+    ids[4, -1] = cfg.eos_token_id                  # EOS only in the last slot: every row live
+    cases = [torch.from_numpy(ids).cuda(), torch.from_numpy(ids[:9, :13].copy()).cuda()]
+    imgs = torch.from_numpy(syn.images_u8(5, cfg.image_size, 78)).cuda()
+    outs = {}
+    try:
+        for flag in (0, 32, 8, 40):
+            C.lib().clm_debug_set(flag)
+            res = [m.encode_ids(x) for x in cases]
+            for split in (1, 2):
+                oi = torch.empty((5, cfg.proj_dim), device="cuda")
+                ot = torch.empty((61, cfg.proj_dim), device="cuda")
+                m.encode_pair(imgs, cases[0], out_img=oi, out_txt=ot, graph=(split == 2), split=split)
+                torch.cuda.synchronize()
+                res.append(ot.clone())
+            outs[flag] = res
+    finally:
+        C.lib().clm_debug_set(0)
+    for flag in (32, 8, 40):
+        for i, (a, b) in enumerate(zip(outs[0], outs[flag])):
+            if flag == 8 or flag == 40:   # every-row last layer vs pruned (split-K pooled GEMMs): fp32 rounding
+                assert torch.max(torch.abs(a - b)).item() <= 1e-5, (flag, i)
+            else:
+                assert torch.equal(a, b), f"case {i}: varlen vs padded max diff {(a - b).abs().max().item():.3e}"
+    for i, (a, b) in enumerate(zip(outs[8], outs[40])):
+        assert torch.equal(a, b), f"every-row case {i}: varlen vs padded"
