@@ -275,7 +275,8 @@ thread_local bool g_concurrent = false;
 template <int NM>
 int pick_from(const CfgModel (&models)[NM], int M, int N) {
   static const long long env_skip = getenv("CLM_GEMM_SKIP_MASK") ? atoll(getenv("CLM_GEMM_SKIP_MASK")) : 0;   // A/B: bit per config id
-  const long long skip = env_skip | (g_concurrent ? (1LL << 24) : 0);
+  static const bool conc_tiles = !(getenv("CLM_CONC_TILES") && !atoi(getenv("CLM_CONC_TILES")));   // A/B switch
+  const long long skip = env_skip | (g_concurrent && conc_tiles ? (1LL << 24) : 0);
   int best = models[0].id;
   double best_cost = 1e300;
   for (const CfgModel& c : models) {
