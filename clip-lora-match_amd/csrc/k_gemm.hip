@@ -321,6 +321,10 @@ int pick_config(int epi, int M, int N) {
     stages = e ? atoi(e) : 2;
   }
   if (!((g2_epis >> epi) & 1)) return pick_from(MODELS, M, N);
+  // Large M (>= 4 full rounds of 256 x 256 tiles, e.g. ViT-L/14@336 batch 128: fc1 73,856 x 4,096):
+  // quantisation no longer favours G2's narrower tiles: gemm_kernel 256 x 256 takes 636 us there
+  // against 874 for G2 256 x 128 (tools/quant_probe.py, profiles/r02_v6_l14_gemm_probe.txt)
+  if (epi == EPI_GELU && (int64_t)((M + 255) / 256) * ((N + 255) / 256) >= 4 * 256) return 4;
   const int id = pick_from(MODELS_G2, M, N);
   if (stages == 3) return id == 16 ? 21 : id == 18 ? 22 : id;
   if (defer && (epi == EPI_STORE || epi == EPI_GELU)) return id == 16 ? 19 : id == 18 ? 20 : id;

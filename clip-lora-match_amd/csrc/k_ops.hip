@@ -183,6 +183,25 @@ __global__ __launch_bounds__(256) void ln4_kernel(LnArgs aa) {
     if (a.mode == 1) store_h();
     ln(a.g1, a.b1);
   }
+  if (!a.loraA && row0 + 1 < a.M && (a.ldy % 8) == 0) {
+    // 16-B stores for the wave's two rows: lane pairs (2l, 2l+1) swap one 8-B half by DPP, then
+    // the even lane stores row 0's 8 consecutive values, the odd lane row 1's (one store
+    // instruction per chunk for both rows instead of two 8-B ones; same values)
+    const bool odd = lane & 1;
+    u16* y0 = a.y + (int64_t)row0 * a.ldy;
+#pragma unroll
+    for (int i = 0; i < NQ; ++i) {
+      const u32x2 p0{pack2<BF>(x[0][i].x, x[0][i].y), pack2<BF>(x[0][i].z, x[0][i].w)};
+      const u32x2 p1{pack2<BF>(x[1][i].x, x[1][i].y), pack2<BF>(x[1][i].z, x[1][i].w)};
+      const u32x2 snd = odd ? p0 : p1;
+      const u32x2 rcv{(uint32_t)__builtin_amdgcn_update_dpp(0, (int)snd.x, 0xB1, 0xF, 0xF, false),
+                      (uint32_t)__builtin_amdgcn_update_dpp(0, (int)snd.y, 0xB1, 0xF, 0xF, false)};
+      const int e = (i * 64 + (lane & ~1)) * 4;   // the pair's first column
+      if (!odd) *(u32x4*)(y0 + e) = u32x4{p0.x, p0.y, rcv.x, rcv.y};
+      else *(u32x4*)(y0 + a.ldy + e) = u32x4{rcv.x, rcv.y, p1.x, p1.y};
+    }
+    return;
+  }
 #pragma unroll
   for (int r = 0; r < R; ++r) {
     if (row0 + r >= a.M) break;
