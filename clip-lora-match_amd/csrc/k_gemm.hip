@@ -358,6 +358,26 @@ hipError_t gemm_cfg(bool bf16, int epi, int config, const GemmArgs& g, hipStream
 
 hipError_t gemm(bool bf16, int epi, const GemmArgs& g, hipStream_t s) {
   if (g.ksplit > 1) return hipErrorInvalidValue;   // split-K: gemm_splitk_resid only
+  // $CLM_GEMM_MSPLIT=1 (experiment, off: 4 % slower in the two-tower pipeline, whose other tower
+  // already fills a partial round; profiles/r02_v6_gemm_msplit_ab.txt): a quick-GELU GEMM whose 256 x 256 tiles fill at least one
+  // full round of the 256 CUs runs as two launches on the same stream -- the row panels of the
+  // full rounds with gemm_kernel 256 x 256, the remaining rows with the heuristic's tile -- so
+  // the last, partial round is of smaller tiles. Rows are independent and every tile config
+  // gives the same bits, so the results are unchanged.
+  static const bool msplit = getenv("CLM_GEMM_MSPLIT") && atoi(getenv("CLM_GEMM_MSPLIT"));
+  if (msplit && epi == EPI_GELU && !g.m_dev && g.M > 0 && g.N > 0) {
+    const int64_t ntn = (g.N + 255) / 256, ntm = (g.M + 255) / 256, tiles = ntn * ntm;
+    const int64_t M1 = (tiles / 256) * 256 / ntn * 256;   // whole 256-row panels of the full rounds
+    if (M1 > 0 && M1 < g.M && tiles % 256) {
+      GemmArgs a = g, b = g;
+      a.M = (int)M1;
+      b.M = g.M - (int)M1;
+      b.A = g.A + M1 * g.lda;
+      b.out = (u16*)g.out + M1 * g.ldo;
+      hipError_t e = gemm_cfg(bf16, epi, 4, a, s);
+      return e != hipSuccess ? e : gemm_cfg(bf16, epi, -1, b, s);
+    }
+  }
   return gemm_cfg(bf16, epi, -1, g, s);
 }
 
