@@ -185,7 +185,9 @@ int clm_gemm_num_configs(void);
  * $CLM_GEMM_DEBUG: for later clm_gemm calls bit 0 = skip the epilogue (accumulators kept
  * live), bit 1 = run the epilogue but drop every store, bit 2 = one tile per workgroup
  * instead of the persistent grid; for later encodes bit 3 (value 8) = run the last encoder
- * layer on every row instead of only the pooled rows (same embeddings, for parity tests). */
+ * layer on every row instead of only the pooled rows, bit 4 (16) = q/k/v GEMM and attention
+ * as two kernels instead of the fused one, bit 5 (32) = encode every padded caption row
+ * instead of each caption's live rows (all: same embeddings, for parity tests). */
 void clm_debug_set(int flags);
 /* attention over qkv [B*T, 3*H*64] (q pre-scaled), out [B*T, ldo] (device pointers) */
 int clm_attention(int hip_device, int dtype, int causal, const void* qkv, void* out, int64_t ldo,
