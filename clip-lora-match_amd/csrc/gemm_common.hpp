@@ -19,7 +19,37 @@ inline int grid_pct() {
   }
   return pct;
 }
+// banded persistent tile walk (tile_walk below), $CLM_GEMM_BAND=1; off by default: it left the
+// GEMMs' L2 hit rate (71-86 %) and the pair step unchanged (profiles/r02_v6_gemm_band_ab.txt)
+inline int gemm_band() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("CLM_GEMM_BAND");
+    v = (e && atoi(e)) ? 1 : 0;
+  }
+  return v;
+}
 constexpr int BK = 64;
+
+// Persistent tile walk of workgroup blockIdx.x over `ntiles` tiles with G workgroups.
+// Banded (GemmArgs::band, $CLM_GEMM_BAND=1): the tile order is cut into 8 contiguous bands, one per XCD
+// group (blocks b = x mod 8 share an XCD under the round-robin dispatch; which XCD is not assumed,
+// only that they share one -- a wrong guess costs speed, never correctness), and the group's
+// workgroups walk their band round by round, so each XCD's L2 keeps serving the same row-panel
+// group instead of every XCD sweeping the whole tile space. Otherwise workgroup xb (the bijective
+// XCD remap) takes tiles xb, xb + G, ...
+struct TileWalk { int first, stride, count; };
+__device__ __forceinline__ TileWalk tile_walk(int ntiles, int G, bool band) {
+  if (band && G >= 8) {
+    const int x = blockIdx.x % 8, j = blockIdx.x / 8;
+    const int nx = (G - x + 7) / 8;   // workgroups of this XCD group
+    const int lo = (int)((int64_t)ntiles * x / 8), hi = (int)((int64_t)ntiles * (x + 1) / 8);
+    const int n = hi - lo;
+    return TileWalk{lo + j, nx, j < n ? (n - j + nx - 1) / nx : 0};
+  }
+  const int xb = xcd_remap(blockIdx.x, G);
+  return TileWalk{xb, G, xb < ntiles ? (ntiles - 1 - xb) / G + 1 : 0};
+}
 
 template <int BM, int BN, int WM, int WN, int STAGES>
 struct Cfg {

@@ -29,8 +29,8 @@ namespace clm {
 
 namespace {
 using namespace gemm_detail;
-// Persistent: workgroup b takes tiles xb, xb + G, xb + 2G, ... (G = gridDim.x <= tiles,
-// xb = XCD-aware remap of b), and its LDS-DMA ring runs ACROSS tile boundaries: the first
+// Persistent: workgroup b walks its tiles (tile_walk: one contiguous band per XCD group, G =
+// gridDim.x <= tiles workgroups), and its LDS-DMA ring runs ACROSS tile boundaries: the first
 // K-tiles of tile i+1 are issued before tile i's epilogue, so they land while the epilogue
 // runs, and the epilogue's stores drain under tile i+1's main loop (counted vmcnt that
 // leaves them in flight). A one-tile-per-workgroup grid is the plain non-persistent GEMM.
@@ -45,14 +45,14 @@ __global__ __launch_bounds__(WM * WN * 64, (Cfg<BM, BN, WM, WN, STAGES>::WAVES_P
   const int ntn = (g.N + BN - 1) / BN, ntm = (g.M + BM - 1) / BM;
   const int ks = g.ksplit > 1 ? g.ksplit : 1;   // split-K: work unit = (tile, K slice)
   const int ntiles = ntn * ntm * ks, G = gridDim.x;
-  const int xb = xcd_remap(blockIdx.x, G);
-  if (xb >= ntiles) return;   // varlen: fewer live tiles than the grid
-  const int n_my = (ntiles - 1 - xb) / G + 1;
+  const TileWalk tw = tile_walk(ntiles, G, g.band != 0);
+  if (tw.count <= 0) return;   // varlen: fewer live tiles than the grid
+  const int n_my = tw.count;
   const int nk = g.K / BK / ks;
   const int S = n_my * nk;   // K-steps of all this workgroup's tiles, one ring
 
   auto coords = [&](int i, int& m0, int& n0, int& k0) {
-    int t = i * G + xb;
+    int t = tw.first + i * tw.stride;
     k0 = 0;
     if (ks > 1) {   // the slices of one tile are adjacent units (same XCD under the remap)
       k0 = (t % ks) * nk * BK;
@@ -212,7 +212,9 @@ hipError_t launch_cfg(const GemmArgs& g, hipStream_t s) {
   }
   const int tiles = ((g.N + BN - 1) / BN) * ((g.M + BM - 1) / BM) * (g.ksplit > 1 ? g.ksplit : 1);
   const int nwg = (g.debug & 4) ? tiles : std::min(tiles, std::max(1, sl * grid_pct() / 100));   // debug bit 2: one tile per workgroup
-  kern<<<dim3(nwg), dim3(C::NT), C::LDS, s>>>(g);
+  GemmArgs ga = g;
+  ga.band = gemm_band();
+  kern<<<dim3(nwg), dim3(C::NT), C::LDS, s>>>(ga);
   return hipGetLastError();
 }
 

@@ -48,14 +48,14 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void gemm2_kernel(GemmArgs ga) {
   const int wm = wid / WN, wn = wid % WN;
   const int ntn = (g.N + BN - 1) / BN, ntm = (g.M + BM - 1) / BM;
   const int ntiles = ntn * ntm, G = gridDim.x;
-  const int xb = xcd_remap(blockIdx.x, G);
-  if (xb >= ntiles) return;   // varlen: fewer live tiles than the grid
-  const int n_my = (ntiles - 1 - xb) / G + 1;
+  const TileWalk tw = tile_walk(ntiles, G, g.band != 0);
+  if (tw.count <= 0) return;   // varlen: fewer live tiles than the grid
+  const int n_my = tw.count;
   const int nk = g.K / BK;
   const int S = n_my * nk;
 
   auto coords = [&](int i, int& m0, int& n0) {
-    const int t = i * G + xb;
+    const int t = tw.first + i * tw.stride;
     int tm, tn;
     if (g.m_fastest) {
       tm = t % ntm;
@@ -277,7 +277,9 @@ hipError_t launch_cfg2(const GemmArgs& g, hipStream_t s) {
   }
   const int tiles = ((g.N + BN - 1) / BN) * ((g.M + BM - 1) / BM);
   const int nwg = (g.debug & 4) ? tiles : std::min(tiles, std::max(1, cus * grid_pct() / 100));   // <= one per CU
-  kern<<<dim3(nwg), dim3(C::NT), C::LDS, s>>>(g);
+  GemmArgs ga = g;
+  ga.band = gemm_band();
+  kern<<<dim3(nwg), dim3(C::NT), C::LDS, s>>>(ga);
   return hipGetLastError();
 }
 

@@ -50,6 +50,7 @@ struct GemmArgs {
   // varlen rows (packed text tower): if set, the row count is *m_dev (device-resident, <= M, which
   // sizes the grid), so a captured graph replays with data-dependent row counts
   const int* m_dev;
+  int band;        // persistent tile walk in one band per XCD group (gemm_common.hpp tile_walk); set by the launcher
   int debug;       // diagnostics only: 1 = skip the epilogue (accumulators kept live), 2 = drop its
                    // stores, 4 = one tile per workgroup (non-persistent grid)
 };
