@@ -1469,13 +1469,16 @@ static int search_bounded(clm_index* x, bool sampled, int64_t S, const u16* q16,
   // path's block is bounded by its sample-score matrix (nqb x S fp32): at most $CLM_SEARCH_WS_MB
   // (default 8192) and at most a quarter of the free HBM.
   static const int64_t ws_mb = getenv("CLM_SEARCH_WS_MB") ? atoll(getenv("CLM_SEARCH_WS_MB")) : 8192;
-  int64_t nqb = std::min<int64_t>(nq, 4096);
+  // query-block cap ($CLM_SEARCH_QB, A/B): a block's fp16 queries are re-read from L2 by every
+  // index tile, so 4096 x 512 (4 MB) fills an XCD's L2
+  static const int64_t qb_cap = getenv("CLM_SEARCH_QB") ? std::max<int64_t>(64, atoll(getenv("CLM_SEARCH_QB"))) : 4096;
+  int64_t nqb = std::min<int64_t>(nq, qb_cap);
   if (sampled) {
     size_t fr = 0, tot = 0;
     int64_t cap_b = ws_mb << 20;
     if (hipMemGetInfo(&fr, &tot) == hipSuccess) cap_b = std::min<int64_t>(cap_b, (int64_t)(fr / 4));
     else (void)hipGetLastError();
-    nqb = std::min<int64_t>(nq, std::max<int64_t>(256, cap_b / ((int64_t)S * 4)));
+    nqb = std::min<int64_t>(std::min<int64_t>(nq, qb_cap), std::max<int64_t>(256, cap_b / ((int64_t)S * 4)));
   }
   size_t off = 0;
   auto take = [&](size_t bytes) { size_t o = off; off = round_up(off + bytes, 256); return o; };
