@@ -7,6 +7,12 @@
 
 #include "kernels.hpp"
 
+// cache policy of the epilogue's output stores (experiment build -DCLM_STORE_AUX=16: sc1, which
+// writes through and drops the line from the XCD's L2 instead of keeping it)
+#ifndef CLM_STORE_AUX
+#define CLM_STORE_AUX 0
+#endif
+
 namespace clm {
 namespace gemm_detail {
 // percentage of the resident workgroup slots a persistent GEMM grid takes ($CLM_GEMM_GRID_PCT,
@@ -206,7 +212,7 @@ __device__ __forceinline__ void epilogue(const GemmArgs& g, const f32x4 (&acc)[B
           const auto ry = __builtin_amdgcn_permlane16_swap(p0.y, p1.y, false, false);
           const int col = wcol8 + nb * 16;
           const uint32_t off = (m < g.M && col < g.N) ? (uint32_t)(((m - m0) * g.ldo + col) * 2) : BUF_OOB;
-          __builtin_amdgcn_raw_buffer_store_b128(u32x4{rx[0], ry[0], rx[1], ry[1]}, ob, off, 0, 0);
+          __builtin_amdgcn_raw_buffer_store_b128(u32x4{rx[0], ry[0], rx[1], ry[1]}, ob, off, 0, CLM_STORE_AUX);
         }
       }
     } else {
@@ -217,7 +223,7 @@ __device__ __forceinline__ void epilogue(const GemmArgs& g, const f32x4 (&acc)[B
         for (int nb = 0; nb < C::TN; ++nb) {
           const int n = wcol + nb * 16;
           const uint32_t off = (m < g.M && n < g.N) ? (uint32_t)(((m - m0) * g.ldo + n) * 2) : BUF_OOB;
-          __builtin_amdgcn_raw_buffer_store_b64(finish(mb, nb), ob, off, 0, 0);
+          __builtin_amdgcn_raw_buffer_store_b64(finish(mb, nb), ob, off, 0, CLM_STORE_AUX);
         }
       }
     }
@@ -284,7 +290,8 @@ __device__ __forceinline__ void epilogue(const GemmArgs& g, const f32x4 (&acc)[B
         const float r2 = __uint_as_float(hc[nb][2]) + (acc[mb][nb][2] + c.z);
         const float r3 = __uint_as_float(hc[nb][3]) + (acc[mb][nb][3] + c.w);
         __builtin_amdgcn_raw_buffer_store_b128(
-            u32x4{__float_as_uint(r0), __float_as_uint(r1), __float_as_uint(r2), __float_as_uint(r3)}, ob, oo, 0, 0);
+            u32x4{__float_as_uint(r0), __float_as_uint(r1), __float_as_uint(r2), __float_as_uint(r3)}, ob, oo, 0,
+            CLM_STORE_AUX);
         if (st) {
           // 16-B stores of the 16-bit copy: as the STORE epilogue's wide path, v_permlane16_swap
           // gives lane group q the 8 consecutive columns (nb-1 + (q & 1)) * 16 + (q >> 1) * 8 ..
