@@ -35,6 +35,18 @@ inline int gemm_band() {
   }
   return v;
 }
+// grouped-raster row panels per group ($CLM_GEMM_GM). 4: an XCD's 32 concurrent tiles cover 4
+// row panels x 8 column tiles, fewer unique operand bytes per round than 8 x 4 (Infinity-Cache
+// traffic is the main loops' bound): pair step +0.9 % vs 8, 16 -3.7 %, 2 +0.2 %
+// (profiles/r02_v6_gemm_raster_ab.txt)
+inline int gemm_gm() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("CLM_GEMM_GM");
+    v = e ? std::max(1, std::min(64, atoi(e))) : 4;
+  }
+  return v;
+}
 constexpr int BK = 64;
 
 // Persistent tile walk of workgroup blockIdx.x over `ntiles` tiles with G workgroups.

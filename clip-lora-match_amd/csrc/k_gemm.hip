@@ -63,7 +63,7 @@ __global__ __launch_bounds__(WM * WN * 64, (Cfg<BM, BN, WM, WN, STAGES>::WAVES_P
       tm = t % ntm;
       tn = t / ntm;
     } else {                    // grouped raster: GM row-panels x all N-tiles per group, M inner,
-      constexpr int GM = 8;     // so an XCD's concurrent tiles share A panels and W tiles in L2
+      const int GM = g.gm > 0 ? g.gm : 4;     // so an XCD's concurrent tiles share A panels and W tiles in L2
       const int group = t / (GM * ntn);
       const int first_m = group * GM;
       const int gsz = min(GM, ntm - first_m);
@@ -214,6 +214,7 @@ hipError_t launch_cfg(const GemmArgs& g, hipStream_t s) {
   const int nwg = (g.debug & 4) ? tiles : std::min(tiles, std::max(1, sl * grid_pct() / 100));   // debug bit 2: one tile per workgroup
   GemmArgs ga = g;
   ga.band = gemm_band();
+  ga.gm = gemm_gm();
   kern<<<dim3(nwg), dim3(C::NT), C::LDS, s>>>(ga);
   return hipGetLastError();
 }

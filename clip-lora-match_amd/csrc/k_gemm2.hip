@@ -61,7 +61,7 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void gemm2_kernel(GemmArgs ga) {
       tm = t % ntm;
       tn = t / ntm;
     } else {
-      constexpr int GM = 8;
+      const int GM = g.gm > 0 ? g.gm : 4;
       const int group = t / (GM * ntn);
       const int first_m = group * GM;
       const int gsz = min(GM, ntm - first_m);
@@ -279,6 +279,7 @@ hipError_t launch_cfg2(const GemmArgs& g, hipStream_t s) {
   const int nwg = (g.debug & 4) ? tiles : std::min(tiles, std::max(1, cus * grid_pct() / 100));   // <= one per CU
   GemmArgs ga = g;
   ga.band = gemm_band();
+  ga.gm = gemm_gm();
   kern<<<dim3(nwg), dim3(C::NT), C::LDS, s>>>(ga);
   return hipGetLastError();
 }

@@ -51,6 +51,7 @@ struct GemmArgs {
   // sizes the grid), so a captured graph replays with data-dependent row counts
   const int* m_dev;
   int band;        // persistent tile walk in one band per XCD group (gemm_common.hpp tile_walk); set by the launcher
+  int gm;          // grouped raster: row panels per group (0 = 4); set by the launcher ($CLM_GEMM_GM)
   int debug;       // diagnostics only: 1 = skip the epilogue (accumulators kept live), 2 = drop its
                    // stores, 4 = one tile per workgroup (non-persistent grid)
 };
