@@ -105,13 +105,13 @@ __global__ __launch_bounds__(256) void ln_kernel(LnArgs aa) {
 
 // d % 256 == 0: lane owns NQ float4 at e = (i*64 + lane)*4 (16-B loads, 8-B bf16 stores: half
 // the memory instructions of the float2 form above; HBM-bound).
-template <bool BF, int NQ>
+template <bool BF, int NQ, int R = 2>
 __global__ __launch_bounds__(256) void ln4_kernel(LnArgs aa) {
   LnArgs a = aa;   // varlen: the device-resident row count (the grid was sized for aa.M)
   if (a.m_dev) a.M = __builtin_amdgcn_readfirstlane(*a.m_dev);
-  // R rows per wave (both rows' loads issued before either is reduced; gamma / beta loaded
-  // once per wave and reused)
-  constexpr int R = 2;
+  // R rows per wave (every row's loads issued before any is reduced; gamma / beta loaded
+  // once per wave and reused); the 16-B paired store path below takes rows in pairs
+  static_assert(R % 2 == 0, "rows per wave come in pairs");
   const int lane = threadIdx.x & 63;
   const int row0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * R;
   if (row0 >= a.M) return;
@@ -183,22 +183,25 @@ __global__ __launch_bounds__(256) void ln4_kernel(LnArgs aa) {
     if (a.mode == 1) store_h();
     ln(a.g1, a.b1);
   }
-  if (!a.loraA && row0 + 1 < a.M && (a.ldy % 8) == 0) {
-    // 16-B stores for the wave's two rows: lane pairs (2l, 2l+1) swap one 8-B half by DPP, then
-    // the even lane stores row 0's 8 consecutive values, the odd lane row 1's (one store
-    // instruction per chunk for both rows instead of two 8-B ones; same values)
+  if (!a.loraA && row0 + R - 1 < a.M && (a.ldy % 8) == 0) {
+    // 16-B stores for each pair of the wave's rows: lane pairs (2l, 2l+1) swap one 8-B half by
+    // DPP, then the even lane stores row 0's 8 consecutive values, the odd lane row 1's (one
+    // store instruction per chunk for both rows instead of two 8-B ones; same values)
     const bool odd = lane & 1;
-    u16* y0 = a.y + (int64_t)row0 * a.ldy;
 #pragma unroll
-    for (int i = 0; i < NQ; ++i) {
-      const u32x2 p0{pack2<BF>(x[0][i].x, x[0][i].y), pack2<BF>(x[0][i].z, x[0][i].w)};
-      const u32x2 p1{pack2<BF>(x[1][i].x, x[1][i].y), pack2<BF>(x[1][i].z, x[1][i].w)};
-      const u32x2 snd = odd ? p0 : p1;
-      const u32x2 rcv{(uint32_t)__builtin_amdgcn_update_dpp(0, (int)snd.x, 0xB1, 0xF, 0xF, false),
-                      (uint32_t)__builtin_amdgcn_update_dpp(0, (int)snd.y, 0xB1, 0xF, 0xF, false)};
-      const int e = (i * 64 + (lane & ~1)) * 4;   // the pair's first column
-      if (!odd) *(u32x4*)(y0 + e) = u32x4{p0.x, p0.y, rcv.x, rcv.y};
-      else *(u32x4*)(y0 + a.ldy + e) = u32x4{rcv.x, rcv.y, p1.x, p1.y};
+    for (int r = 0; r < R; r += 2) {
+      u16* y0 = a.y + (int64_t)(row0 + r) * a.ldy;
+#pragma unroll
+      for (int i = 0; i < NQ; ++i) {
+        const u32x2 p0{pack2<BF>(x[r][i].x, x[r][i].y), pack2<BF>(x[r][i].z, x[r][i].w)};
+        const u32x2 p1{pack2<BF>(x[r + 1][i].x, x[r + 1][i].y), pack2<BF>(x[r + 1][i].z, x[r + 1][i].w)};
+        const u32x2 snd = odd ? p0 : p1;
+        const u32x2 rcv{(uint32_t)__builtin_amdgcn_update_dpp(0, (int)snd.x, 0xB1, 0xF, 0xF, false),
+                        (uint32_t)__builtin_amdgcn_update_dpp(0, (int)snd.y, 0xB1, 0xF, 0xF, false)};
+        const int e = (i * 64 + (lane & ~1)) * 4;   // the pair's first column
+        if (!odd) *(u32x4*)(y0 + e) = u32x4{p0.x, p0.y, rcv.x, rcv.y};
+        else *(u32x4*)(y0 + a.ldy + e) = u32x4{rcv.x, rcv.y, p1.x, p1.y};
+      }
     }
     return;
   }
@@ -230,6 +233,19 @@ __global__ __launch_bounds__(256) void ln4_kernel(LnArgs aa) {
 template <bool BF>
 hipError_t ln_dispatch(const LnArgs& a, hipStream_t s) {
   dim3 grid((a.M + 3) / 4), block(256);
+  // ln4_kernel rows per wave: 2 (default) or 4 ($CLM_LN_ROWS=4, A/B: twice the loads in flight
+  // per wave at the same occupancy)
+  static const int rows = (getenv("CLM_LN_ROWS") && atoi(getenv("CLM_LN_ROWS")) == 4) ? 4 : 2;
+  if (rows == 4 && a.d >= 256 && a.d <= 1024 && a.d % 256 == 0) {
+    dim3 grid4((a.M + 15) / 16);
+    switch (a.d) {
+      case 256: ln4_kernel<BF, 1, 4><<<grid4, block, 0, s>>>(a); break;
+      case 512: ln4_kernel<BF, 2, 4><<<grid4, block, 0, s>>>(a); break;
+      case 768: ln4_kernel<BF, 3, 4><<<grid4, block, 0, s>>>(a); break;
+      case 1024: ln4_kernel<BF, 4, 4><<<grid4, block, 0, s>>>(a); break;
+    }
+    return hipGetLastError();
+  }
   dim3 grid2((a.M + 7) / 8);   // ln4_kernel: 2 rows per wave
   switch (a.d) {
     case 128: ln_kernel<BF, 1><<<grid, block, 0, s>>>(a); break;
