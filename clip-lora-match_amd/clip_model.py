@@ -149,12 +149,9 @@ def load_clip_model(
 
 
 def _encode_images(images, model: ClipLoraModel, processor: ClipProcessor, normalize: bool) -> torch.Tensor:
-    u8 = processor.images_u8(images)
-    if u8 is not None:
-        pix = torch.from_numpy(u8).to(model.device, non_blocking=False)
-    else:
-        pix = torch.from_numpy(processor.pixel_values(images)).to(model.device)
-    return model.encode_pixels(pix, normalize=normalize)
+    """host decode -> GPU resize + centre crop (clm_resize_crop) -> GPU encode (uint8 path:
+    rescale / normalise fused in patchify)."""
+    return model.encode_pixels(processor.images_u8(images, model.device), normalize=normalize)
 
 
 def encode_image(

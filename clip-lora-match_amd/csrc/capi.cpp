@@ -1754,3 +1754,133 @@ int clm_fuse_queries(int hip_device, const float* a, float w_a, const float* b, 
 }
 
 }  // extern "C"
+
+// ---------------------------------------------------------------- images ----
+// Tap tables of PIL's 8-bit resampler (Pillow 12.2.0 src/libImaging/Resample.c precompute_coeffs +
+// normalize_coeffs_8bpc, BICUBIC a = -0.5, support 2), the resize CLIPImageProcessor runs
+// (models/clip_model.py:108-110); restated with the same double arithmetic and operation order as
+// oracle/image_ref.py:coeffs. Contraction is off so no FMA can change a weight's last bit.
+namespace {
+#pragma clang fp contract(off)
+double pil_bicubic(double x) {
+  const double a = -0.5;
+  if (x < 0.0) x = -x;
+  if (x < 1.0) return ((a + 2.0) * x - (a + 3.0)) * x * x + 1;
+  if (x < 2.0) return (((x - 5) * x + 8) * x - 4) * a;
+  return 0.0;
+}
+
+// taps of output coordinates [first, first + count) of an in_size -> out_size resample:
+// mins / ns [count] and fixed-point weights [count][ksize]; returns ksize
+int pil_coeffs(int in_size, int out_size, int first, int count, std::vector<int32_t>& mins,
+               std::vector<int32_t>& ns, std::vector<int32_t>& ks) {
+  const double scale = (double)(float)in_size / out_size;
+  const double filterscale = scale < 1.0 ? 1.0 : scale;
+  const double support = 2.0 * filterscale;
+  const int ksize = (int)std::ceil(support) * 2 + 1;
+  mins.assign(count, 0);
+  ns.assign(count, 0);
+  ks.assign((size_t)count * ksize, 0);
+  std::vector<double> w(ksize);
+  for (int i = 0; i < count; ++i) {
+    const int xx = first + i;
+    const double center = (xx + 0.5) * scale;
+    const double ss = 1.0 / filterscale;
+    int xmin = (int)(center - support + 0.5);
+    if (xmin < 0) xmin = 0;
+    int xmax = (int)(center + support + 0.5);
+    if (xmax > in_size) xmax = in_size;
+    xmax -= xmin;
+    double ww = 0.0;
+    for (int x = 0; x < xmax; ++x) {
+      w[x] = pil_bicubic((x + xmin - center + 0.5) * ss);
+      ww += w[x];
+    }
+    for (int x = 0; x < xmax; ++x) {
+      const double k = ww != 0.0 ? w[x] / ww : w[x];
+      ks[(size_t)i * ksize + x] = k < 0 ? (int32_t)(-0.5 + k * (1 << 22)) : (int32_t)(0.5 + k * (1 << 22));
+    }
+    mins[i] = xmin;
+    ns[i] = xmax;
+  }
+  return ksize;
+}
+#pragma clang fp contract(on)
+
+}  // namespace
+
+extern "C" int clm_resize_crop(int hip_device, const uint8_t* src, const int64_t* offs, const int32_t* hw,
+                               int n, int S, uint8_t* out, void* stream) {
+  if (n < 0 || S <= 0 || S > 4096 || (n > 0 && (!src || !offs || !hw || !out)))
+    return fail(CLM_E_ARG, "resize_crop: bad argument");
+  if (n == 0) return CLM_OK;
+  std::vector<ResizeDesc> desc(n);
+  std::vector<int32_t> coef;
+  int64_t src_bytes = 0, tmp_bytes = 0;
+  int max_rows = 0;
+  std::vector<int32_t> xmin, xn, xk, ymin, yn, yk;
+  for (int i = 0; i < n; ++i) {
+    const int H = hw[2 * i], W = hw[2 * i + 1];
+    if (H < 1 || W < 1 || (int64_t)H * W > ((int64_t)1 << 28) || offs[i] < 0)
+      return fail(CLM_E_ARG, "resize_crop: image " + std::to_string(i) + " has a bad size or offset");
+    src_bytes = std::max(src_bytes, offs[i] + (int64_t)H * W * 3);
+    // get_resize_output_image_size(default_to_square=False): short -> S, long -> int(S * long / short)
+    const int shrt = std::min(H, W), lng = std::max(H, W);
+    const int new_long = (int)((double)((int64_t)S * lng) / shrt);
+    const int nh = W <= H ? new_long : S, nw = W <= H ? S : new_long;
+    const int top = (nh - S) / 2, left = (nw - S) / 2;   // center_crop; nh, nw >= S
+    ResizeDesc& d = desc[i];
+    d.src_off = offs[i];
+    d.W = W;
+    d.kh = pil_coeffs(W, nw, left, S, xmin, xn, xk);
+    d.kv = pil_coeffs(H, nh, top, S, ymin, yn, yk);
+    int r1 = 0;
+    for (int y = 0; y < S; ++y) r1 = std::max(r1, ymin[y] + yn[y]);
+    d.r0 = ymin[0];
+    d.rows = r1 - d.r0;
+    for (int y = 0; y < S; ++y) ymin[y] -= d.r0;
+    d.tmp_off = tmp_bytes;
+    tmp_bytes += round_up((int64_t)d.rows * S * 3, 256);
+    max_rows = std::max(max_rows, d.rows);
+    d.coef_off = (int32_t)coef.size();
+    if ((int64_t)coef.size() + 4 * S + (int64_t)S * (d.kh + d.kv) > INT32_MAX)
+      return fail(CLM_E_ARG, "resize_crop: tap tables too large");
+    coef.insert(coef.end(), xmin.begin(), xmin.end());
+    coef.insert(coef.end(), xn.begin(), xn.end());
+    coef.insert(coef.end(), ymin.begin(), ymin.end());
+    coef.insert(coef.end(), yn.begin(), yn.end());
+    coef.insert(coef.end(), xk.begin(), xk.end());
+    coef.insert(coef.end(), yk.begin(), yk.end());
+  }
+  DeviceGuard g(hip_device);
+  hipStream_t st = (hipStream_t)stream;
+  const bool sd = is_device_ptr(src), od = is_device_ptr(out);
+  const size_t out_bytes = (size_t)n * S * S * 3;
+  const size_t b_desc = round_up(sizeof(ResizeDesc) * n, 256), b_coef = round_up(coef.size() * 4, 256);
+  const size_t bytes = b_desc + b_coef + (size_t)tmp_bytes + (sd ? 0 : round_up(src_bytes, 256)) +
+                       (od ? 0 : round_up(out_bytes, 256));
+  uint8_t* w = nullptr;
+  if (hipMalloc(&w, bytes) != hipSuccess) { (void)hipGetLastError(); return fail(CLM_E_OOM, "resize_crop workspace"); }
+  size_t off = 0;
+  auto take = [&](size_t b) { size_t o = off; off = round_up(off + b, 256); return w + o; };
+  ResizeDesc* d_desc = (ResizeDesc*)take(sizeof(ResizeDesc) * n);
+  int32_t* d_coef = (int32_t*)take(coef.size() * 4);
+  uint8_t* d_tmp = take((size_t)tmp_bytes);
+  const uint8_t* d_src = src;
+  uint8_t* d_out = out;
+  hipError_t e = hipMemcpyAsync(d_desc, desc.data(), sizeof(ResizeDesc) * n, hipMemcpyHostToDevice, st);
+  if (e == hipSuccess) e = hipMemcpyAsync(d_coef, coef.data(), coef.size() * 4, hipMemcpyHostToDevice, st);
+  if (e == hipSuccess && !sd) {
+    uint8_t* t = take((size_t)src_bytes);
+    e = hipMemcpyAsync(t, src, (size_t)src_bytes, hipMemcpyHostToDevice, st);
+    d_src = t;
+  }
+  if (!od) d_out = take(out_bytes);
+  if (e == hipSuccess) e = resize_crop(d_src, d_desc, n, S, max_rows, d_coef, d_tmp, d_out, st);
+  if (e == hipSuccess && !od) e = hipMemcpyAsync(out, d_out, out_bytes, hipMemcpyDeviceToHost, st);
+  // the tables live in host vectors and the workspace is freed below: wait for the stream
+  if (e == hipSuccess) e = hipStreamSynchronize(st);
+  (void)hipFree(w);
+  if (e != hipSuccess) return fail(CLM_E_HIP, std::string("resize_crop: ") + hipGetErrorString(e));
+  return CLM_OK;
+}

@@ -105,6 +105,19 @@ hipError_t ln_finalize(const float2* stats, int chunks, int M, float eps, float2
 hipError_t lora_down(bool bf16, u16* X, int64_t ldx, int M, int K, const float* A, int r_ext,
                      int r_pad, hipStream_t s);
 
+// shortest-edge bicubic resize + centre crop (k_image.hip), PIL / CLIPImageProcessor arithmetic.
+// Per image: source HWC RGB bytes at src + src_off (row stride 3 W); the crop needs source rows
+// [r0, r0 + rows), whose horizontally resampled S columns go to tmp + tmp_off ([rows][S][3]).
+// coef + coef_off holds int32 xmin[S] | xn[S] | ymin[S] (relative to r0) | yn[S] | xk[S][kh] |
+// yk[S][kv] (22-bit fixed-point taps).
+struct ResizeDesc {
+  int64_t src_off;
+  int64_t tmp_off;
+  int32_t W, r0, rows, kh, kv, coef_off;
+};
+hipError_t resize_crop(const uint8_t* src, const ResizeDesc* desc, int n, int S, int max_rows,
+                       const int32_t* coef, uint8_t* tmp, uint8_t* out, hipStream_t s);
+
 // patchify + (u8 rescale/normalise via lut | f32 copy) -> P[B*G*G, Kp] (compute dtype)
 hipError_t patchify(bool bf16, const void* pix, int layout, int B, int S, int p, int C,
                     const float* lut /*[C*256]*/, u16* P, int Kp, hipStream_t s);

@@ -1,13 +1,14 @@
 """Host-side CLIPProcessor replacement (the `processor` load_clip_model returns).
 
-Image side (CLIPImageProcessor, config/clip_config.yaml:7-13): for RGB images
-already at image_size^2 the resize and centre-crop are identities, so the raw
-uint8 pixels go to the GPU and rescale/normalise run fused in the patchify
-kernel (bit-identical to the processor's float64-rescale + float32-normalise,
-see oracle/clip_ref.py:preprocess_u8). Any other size is resized/cropped on
-the host by transformers' own CLIPImageProcessor when importable, else by a
-PIL bicubic shortest-edge resize + centre crop, and handed over as float32
-pixel_values.
+Image side (CLIPImageProcessor with the reference's settings, config/clip_config.yaml:7-13;
+models/clip_model.py:105-110, src/embedding/embed_image.py:13-19,36-41): the host only decodes
+(PIL `Image.open(path).convert("RGB")`, the reference's own loader); everything after runs on the
+GPU. Images already image_size^2 go straight to the encoder as uint8 (resize and crop are
+identities); any other size goes through clm_resize_crop (csrc/k_image.hip): shortest-edge
+BICUBIC resize + centre crop with PIL's 8-bit resampling arithmetic, bit-identical to
+CLIPImageProcessor's resize + center_crop. Rescale / normalise then run fused in the encoder's
+patchify kernel (a 3 x 256 float32 LUT, bit-identical to the processor's float64-rescale +
+float32-normalise, see oracle/clip_ref.py:preprocess_u8). transformers is not imported.
 
 Text side: tokenizer.ClipBPETokenizer (CLIP byte-level BPE, host-side) over a local
 vocab.json + merges.txt given via `tokenizer_dir` / $CLM_TOKENIZER_DIR (the CLIP
@@ -17,6 +18,7 @@ exactly as CLIPTokenizer(padding=True) produces.
 """
 from __future__ import annotations
 
+import ctypes
 import os
 from pathlib import Path
 from typing import List, Optional, Sequence, Union
@@ -49,6 +51,7 @@ class ClipProcessor:
     # ------------------------------------------------------------- images --
     @staticmethod
     def load_image(image: ImageLike):
+        """PIL RGB image: the reference's _load_image (embed_image.py:13-19; clip_model.py:102-105)."""
         from PIL import Image
         if isinstance(image, Image.Image):
             return image.convert("RGB")
@@ -59,49 +62,60 @@ class ClipProcessor:
             raise FileNotFoundError(f"Image not found: {p}")
         return Image.open(p).convert("RGB")
 
-    def images_u8(self, images: Sequence[ImageLike]) -> Optional[np.ndarray]:
-        """uint8 [n,S,S,3] when every image is already S x S (fast path), else None."""
-        S = self.image_size
-        out = []
-        for im in images:
-            if isinstance(im, np.ndarray) and im.dtype == np.uint8 and im.shape == (S, S, 3):
-                out.append(im)
-                continue
-            pil = self.load_image(im)
-            if pil.size != (S, S):
-                return None
-            out.append(np.asarray(pil, dtype=np.uint8))
-        return np.stack(out) if out else np.zeros((0, S, S, 3), np.uint8)
+    @classmethod
+    def decode(cls, image: ImageLike) -> np.ndarray:
+        """uint8 [H, W, 3] RGB pixels of one image (host decode only)."""
+        if isinstance(image, np.ndarray) and image.dtype == np.uint8 and image.ndim == 3 and image.shape[2] == 3:
+            return np.ascontiguousarray(image)
+        return np.asarray(cls.load_image(image), dtype=np.uint8)
 
-    def pixel_values(self, images: Sequence[ImageLike]) -> np.ndarray:
-        """float32 [n,3,S,S] exactly as CLIPImageProcessor (resize shortest edge, centre crop,
-        rescale, normalise)."""
-        pils = [self.load_image(im) for im in images]
+    def images_u8(self, images: Sequence[ImageLike], device) -> torch.Tensor:
+        """uint8 [n, S, S, 3] on `device`: the CLIPImageProcessor resize + centre crop of every
+        image (clm_resize_crop for sizes other than S x S), ready for encode_pixels."""
+        from . import _capi
         S = self.image_size
-        try:
-            if self._hf_image is None:
-                from transformers import CLIPImageProcessor
-                self._hf_image = CLIPImageProcessor(size={"shortest_edge": S},
-                                                    crop_size={"height": S, "width": S},
-                                                    image_mean=list(self.mean), image_std=list(self.std))
-            return np.asarray(self._hf_image(images=pils, return_tensors="np")["pixel_values"], np.float32)
-        except ImportError:
-            pass
-        from PIL import Image
-        out = []
-        for im in pils:
-            w, h = im.size
-            if w <= h:
-                nw, nh = S, int(S * h / w)
-            else:
-                nw, nh = int(S * w / h), S
-            im = im.resize((nw, nh), Image.BICUBIC)
-            left, top = (nw - S) // 2, (nh - S) // 2
-            im = im.crop((left, top, left + S, top + S))
-            x = (np.asarray(im, np.float64) * (1.0 / 255.0)).astype(np.float32)
-            x = (x - np.asarray(self.mean, np.float32)) / np.asarray(self.std, np.float32)
-            out.append(x.transpose(2, 0, 1))
-        return np.stack(out).astype(np.float32)
+        device = torch.device(device)
+        arrs = [self.decode(im) for im in images]
+        if all(a.shape[:2] == (S, S) for a in arrs):
+            if not arrs:
+                return torch.zeros((0, S, S, 3), dtype=torch.uint8, device=device)
+            return torch.from_numpy(np.stack(arrs)).to(device)
+        _capi.require_gpu()
+        sizes = np.array([a.shape[0] * a.shape[1] * 3 for a in arrs], np.int64)
+        offs = np.zeros(len(arrs), np.int64)
+        offs[1:] = np.cumsum(sizes)[:-1]
+        flat = torch.empty(int(sizes.sum()), dtype=torch.uint8, pin_memory=True)
+        fv = flat.numpy()
+        for a, o, n in zip(arrs, offs, sizes):
+            fv[o:o + n] = a.reshape(-1)
+        src = flat.to(device, non_blocking=True)
+        hw = np.array([a.shape[:2] for a in arrs], np.int32).reshape(-1)
+        out = torch.empty((len(arrs), S, S, 3), dtype=torch.uint8, device=device)
+        _capi.check(_capi.lib().clm_resize_crop(
+            device.index if device.index is not None else torch.cuda.current_device(), _capi.ptr(src),
+            offs.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)), hw.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)),
+            len(arrs), S, _capi.ptr(out), _capi.stream_of(device)), "resize_crop")
+        return out
+
+    def normalize_lut(self) -> np.ndarray:
+        """float32 [3, 256]: pixel value v of channel c -> float32(float64(v) * (1/255)) then
+        (x - mean[c]) / std[c] in float32, i.e. CLIPImageProcessor's rescale + normalise
+        (TF/image_transforms.py:118-122, 419-439) tabulated per byte value."""
+        x = (np.arange(256, dtype=np.float64) * (1 / 255)).astype(np.float32)
+        m = np.asarray(self.mean, np.float32)[:, None]
+        s = np.asarray(self.std, np.float32)[:, None]
+        return ((x[None, :] - m) / s).astype(np.float32)
+
+    def pixel_values(self, images: Sequence[ImageLike], device=None) -> torch.Tensor:
+        """float32 [n, 3, S, S] exactly as CLIPImageProcessor (resize shortest edge, centre crop,
+        rescale, normalise); computed on the GPU, returned on the CPU."""
+        from . import _capi
+        _capi.require_gpu()
+        dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+        u8 = self.images_u8(images, dev).permute(0, 3, 1, 2).long()      # [n, 3, S, S]
+        lut = torch.from_numpy(self.normalize_lut()).to(dev)
+        ch = torch.arange(3, device=dev).view(1, 3, 1, 1) * 256
+        return lut.view(-1)[u8 + ch].cpu()
 
     # --------------------------------------------------------------- text --
     def token_ids(self, text: Union[str, Sequence[str], Sequence[int], Sequence[Sequence[int]], torch.Tensor],
@@ -140,7 +154,7 @@ class ClipProcessor:
         out = {}
         if images is not None:
             imgs = images if isinstance(images, (list, tuple)) else [images]
-            out["pixel_values"] = torch.from_numpy(self.pixel_values(imgs))
+            out["pixel_values"] = self.pixel_values(imgs)
         if text is not None:
             ids = self.token_ids(text, max_length)
             out["input_ids"] = ids.long()

@@ -20,6 +20,27 @@ def images_u8(n: int, size: int, seed: int = 1234) -> np.ndarray:
     return out
 
 
+# (H, W) of the odd-size image set: tiny, one pixel, square off by one, both aspect orientations,
+# an extreme strip whose resized long edge is 34,458 pixels, and camera-like sizes
+ODD_SIZES = ((46, 36), (1, 1), (2, 7), (225, 225), (260, 300), (224, 500), (500, 224), (13, 2000),
+             (999, 1001), (480, 640), (1599, 899))
+
+
+def odd_images(seed: int = 4242, sizes=ODD_SIZES) -> list:
+    """uint8 [H, W, 3] images at sizes other than 224^2: smooth colour gradients + noise, so the
+    bicubic resample sees both edges and texture (numpy PCG64 seed + i)."""
+    out = []
+    for i, (h, w) in enumerate(sizes):
+        rng = np.random.Generator(np.random.PCG64(seed + i))
+        y = np.linspace(0.0, 1.0, h)[:, None, None]
+        x = np.linspace(0.0, 1.0, w)[None, :, None]
+        phase = rng.uniform(0, 2 * np.pi, size=(1, 1, 3))
+        base = 127.5 + 100.0 * np.sin(6.0 * x + 4.0 * y + phase)
+        noise = rng.normal(0.0, 30.0, size=(h, w, 3))
+        out.append(np.clip(np.rint(base + noise), 0, 255).astype(np.uint8))
+    return out
+
+
 def captions(n: int, L: int, bos: int, eos: int, seed: int = 99, min_len: int = 8) -> np.ndarray:
     rng = np.random.Generator(np.random.PCG64(seed))
     ids = np.full((n, L), eos, np.int32)

@@ -24,6 +24,9 @@
  *   clm_topk_merge             (new) merge of per-shard top-k lists for the
  *                              8-GPU sharded search
  *   clm_l2_normalize           v / ||v||_2 (clip_model.py:116,148; search.py:68,93)
+ *   clm_resize_crop            CLIPProcessor's image resize + centre crop for inputs of any
+ *                              size (clip_model.py:105-110, embed_image.py:36-41;
+ *                              config/clip_config.yaml:7-9)
  *
  * Conventions
  *   - return 0 (CLM_OK) on success, a negative CLM_E_* code on error;
@@ -109,6 +112,14 @@ int clm_set_lora(clm_ctx* ctx, int r, float alpha, uint32_t targets);
 /* n images -> out [n, proj_dim] (CLM_F32 or CLM_F16); normalize != 0 => unit rows */
 int clm_encode_image(clm_ctx* ctx, const void* pixels, int pix_layout, int n, void* out,
                      int out_dtype, int normalize, void* stream);
+/* Shortest-edge BICUBIC resize to S + centre crop S x S of n uint8 RGB images of any size
+ * (H, W >= 1), with PIL's 8-bit resampling arithmetic (the CLIPImageProcessor the reference runs):
+ * out is uint8 [n, S, S, 3], bit-identical to PIL Image.resize + transformers center_crop, and
+ * feeds clm_encode_image(CLM_PIX_U8_HWC). Image i is HWC RGB bytes at src + offs[i] with
+ * hw[2 i] = H, hw[2 i + 1] = W (offs, hw: host arrays). src / out: host or device. Synchronous. */
+int clm_resize_crop(int hip_device, const uint8_t* src, const int64_t* offs, const int32_t* hw, int n,
+                    int S, uint8_t* out, void* stream);
+
 /* ids int32 [n, L] (L <= max_pos; each row holds an EOS) -> out [n, proj_dim] */
 int clm_encode_text(clm_ctx* ctx, const int32_t* ids, int n, int L, void* out, int out_dtype,
                     int normalize, void* stream);

@@ -17,6 +17,17 @@ Search goldens: the reference's own src/embedding/similarity.py top_k_similar
 Gaussian fp16-rounded rows/queries, and on the reference's committed
 data/index/custom_items_index.pt (copied here as a data fixture).
 
+Image-preprocessing goldens (`images`): the reference's 17 committed images
+(data/custom/{images,crops,query_crops}, data/reported/images; 14 distinct files, 36x46 to
+1599x899, one palette PNG) and the seeded odd-size synthetic set (synthetic.odd_images, plus
+"L" and "RGBA" variants), decoded as the reference decodes (PIL open + convert("RGB"),
+models/clip_model.py:105) and preprocessed by transformers' CLIPImageProcessor (its PIL backend,
+the reference's resize + centre-crop), then encoded by CLIPModel + LoRA hooks (B/32, the
+synthetic weights). Stored: sha256 of the decoded pixels and of the float32 pixel_values, and
+the fp32 embeddings. The inputs must reach the GPU box, which has no /root/reference: the 14
+files' encoded bytes (930 KB, the smallest lossless form of their pixels) are the input half of
+this vector set, in ref_images.npz.
+
 Only inputs' seeds and outputs are stored; the weights are regenerated from
 their seeds by the tests.
 """
@@ -67,6 +78,62 @@ def encoder_golden(name, preset, n_img, n_txt, L, lora_on, img_seed=1234, cap_se
         out.update(emb_img_base=fi0, emb_txt_base=ft0)
     np.savez_compressed(os.path.join(HERE, name), **out)
     print(f"{name}: img {fi.shape} txt {ft.shape}")
+
+
+REF_IMAGE_DIRS = ("data/custom/images", "data/custom/crops", "data/custom/query_crops", "data/reported/images")
+
+
+def _sha(a: np.ndarray) -> str:
+    import hashlib
+    return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
+
+
+def image_golden():
+    """ref_images.npz (inputs) + enc_b32_lora_images.npz (expected outputs); see module doc."""
+    import hashlib
+    import io
+    import glob
+    from PIL import Image
+    from oracle import clip_ref as R
+    from oracle import image_ref as IR
+    names, blobs, files = [], {}, []
+    for d in REF_IMAGE_DIRS:
+        for f in sorted(glob.glob(os.path.join(REF, d, "*"))):
+            if f.lower().endswith((".jpg", ".jpeg", ".png")):
+                raw = open(f, "rb").read()
+                key = hashlib.sha256(raw).hexdigest()[:16]
+                blobs.setdefault(key, np.frombuffer(raw, np.uint8))
+                names.append(os.path.relpath(f, REF))
+                files.append(key)
+    np.savez_compressed(os.path.join(HERE, "ref_images.npz"), names=np.array(names), keys=np.array(files),
+                        **{"blob_" + k: v for k, v in blobs.items()})
+    cfg = clm.get_preset("ViT-B/32")
+    sd, lora = W.synthetic_state_dict(cfg, 0), W.synthetic_lora(cfg, 1)
+    pils = [Image.open(io.BytesIO(blobs[k].tobytes())).convert("RGB") for k in files]
+    odd = syn.odd_images()
+    pils += [Image.fromarray(a) for a in odd]
+    pils += [Image.fromarray(odd[4]).convert("L").convert("RGB"),
+             Image.fromarray(np.dstack([odd[9], odd[9][..., :1]])).convert("RGB")]
+    labels = names + [f"odd{i}" for i in range(len(odd))] + ["odd4_L", "odd9_RGBA"]
+    from transformers import CLIPImageProcessor
+    proc = CLIPImageProcessor(size={"shortest_edge": cfg.image_size},
+                              crop_size={"height": cfg.image_size, "width": cfg.image_size})
+    pv = np.concatenate([proc(images=[p], return_tensors="np")["pixel_values"] for p in pils]).astype(np.float32)
+    dec = [np.asarray(p, np.uint8) for p in pils]
+    for i, a in enumerate(dec):   # the oracle restatement must reproduce the processor bit for bit
+        mine = R.preprocess_u8(IR.resize_crop_u8(a, cfg.image_size)[None], cfg.mean, cfg.std)[0]
+        assert mine.tobytes() == pv[i].tobytes(), labels[i]
+    m = H.hf_model(cfg, sd, lora)
+    embs = []
+    with torch.no_grad():
+        for i in range(0, len(pv), 8):
+            f = m.get_image_features(pixel_values=torch.from_numpy(pv[i:i + 8])).pooler_output
+            embs.append((f / f.norm(dim=-1, keepdim=True)).numpy())
+    np.savez_compressed(os.path.join(HERE, "enc_b32_lora_images.npz"), labels=np.array(labels),
+                        n_ref=np.array(len(names)), hw=np.array([a.shape[:2] for a in dec], np.int64),
+                        dec_sha=np.array([_sha(a) for a in dec]), pv_sha=np.array([_sha(p) for p in pv]),
+                        emb_img=np.concatenate(embs).astype(np.float32), odd_seed=np.array(4242))
+    print(f"ref_images.npz: {len(blobs)} files for {len(names)} names; enc_b32_lora_images.npz: {len(labels)} images")
 
 
 def _load_ref_similarity():
@@ -134,7 +201,7 @@ def search_fp32_golden():
 
 
 if __name__ == "__main__":
-    which = sys.argv[1:] or ["tiny", "b32", "l14", "search", "search_fp32"]
+    which = sys.argv[1:] or ["tiny", "b32", "l14", "search", "search_fp32", "images"]
     if "tiny" in which:
         encoder_golden("enc_tiny_lora.npz", "tiny", 4, 4, 16, True)
     if "b32" in which:
@@ -145,3 +212,5 @@ if __name__ == "__main__":
         search_golden()
     if "search_fp32" in which:
         search_fp32_golden()
+    if "images" in which:
+        image_golden()

@@ -178,7 +178,7 @@ def test_embed_image_and_batch(tmp_path):
     np.testing.assert_allclose((raw / raw.norm(dim=-1, keepdim=True)).numpy(), eb.numpy(), atol=1e-6)
     empty = embed_images_batch(model, proc, [], dev)
     assert empty.shape == (0,)
-    # non-224 inputs go through the host resize / centre-crop path
+    # non-224 inputs go through the GPU resize / centre-crop path (tests/test_gpu_image.py checks its bits)
     big = Image.fromarray(syn.images_u8(1, 300, 5)[0]).resize((300, 260))
     assert embed_image(model, proc, big, dev).shape == (512,)
     with pytest.raises(FileNotFoundError):

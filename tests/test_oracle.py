@@ -117,3 +117,34 @@ def test_search_oracle_vs_reference_fp32_golden(name, k):
     if name == "clus" and k == 10:   # the fixture is non-trivial: neighbours closer than fp16 resolution
         gaps = -np.diff(vals, axis=1)
         assert np.median(gaps) < 1e-4
+
+
+def test_image_oracle_reproduces_clip_image_processor_golden():
+    """oracle.image_ref (PIL's bicubic resample restated + transformers' size / crop rules) gives
+    the pixel_values CLIPImageProcessor produced for the reference's 17 committed images and the
+    odd-size synthetic set, bit for bit (sha256 of the float32 pixel_values)."""
+    from golden_images import pil_images, sha
+    from oracle import image_ref as IR
+    g = golden("enc_b32_lora_images.npz")
+    cfg = clm.get_preset("ViT-B/32")
+    labels, pils = pil_images()
+    for i, (lab, im) in enumerate(zip(labels, pils)):
+        a = np.asarray(im, np.uint8)
+        assert sha(a) == str(g["dec_sha"][i]), f"{lab}: decoded pixels differ from the golden's"
+        crop = IR.resize_crop_u8(a, cfg.image_size)
+        assert sha(R.preprocess_u8(crop[None], cfg.mean, cfg.std)[0]) == str(g["pv_sha"][i]), lab
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_image_oracle_equals_pil_resize(seed):
+    """the numpy restatement of Resample.c vs Pillow itself, random sizes and both schedules"""
+    from PIL import Image
+    from oracle import image_ref as IR
+    rng = np.random.default_rng(seed)
+    for _ in range(12):
+        h, w = (int(v) for v in rng.integers(1, 400, 2))
+        a = rng.integers(0, 256, (h, w, 3), dtype=np.uint8)
+        nh, nw = IR.shortest_edge_size(h, w, 224)
+        pil = np.asarray(Image.fromarray(a).resize((nw, nh), Image.BICUBIC))
+        assert np.array_equal(IR.resize_bicubic(a, nw, nh), pil), (h, w)
+        assert np.array_equal(IR.resize_crop_u8_window(a, 224), IR.resize_crop_u8(a, 224)), (h, w)
