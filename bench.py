@@ -75,6 +75,10 @@ def parse_args(argv=None):
     ap.add_argument("--no-l14", action="store_true", help="skip the ViT-L/14@336 (configs[3]) leg")
     ap.add_argument("--no-parity-mode", action="store_true", help="skip the fp16 parity-mode step")
     ap.add_argument("--no-varlen", action="store_true", help="skip the mixed-length caption (varlen) leg")
+    ap.add_argument("--no-unmerged", action="store_true", help="skip the unmerged (hot-swappable) LoRA leg")
+    ap.add_argument("--no-index-build", action="store_true", help="skip the configs[2] index-build leg")
+    ap.add_argument("--index-images", type=int, default=1_000_000, help="images of the configs[2] index build")
+    ap.add_argument("--index-batch", type=int, default=512)
     ap.add_argument("--sequential", action="store_true", help="towers back to back on one stream, no graph")
     ap.add_argument("--split", type=int, default=0, help="sub-batches per tower in encode_pair (0 = library default)")
     return ap.parse_args(argv)
@@ -236,9 +240,20 @@ def cpu_search_baseline(host16: torch.Tensor, queries16: torch.Tensor, k: int, m
     dt = time.perf_counter() - t0
     del E
     return {"qps": round(done / dt, 3), "ms_per_query": round(dt / done * 1e3, 2), "queries": done,
+            "sample": f"the first {done} of {queries16.shape[0]} queries, one at a time (a {budget_s:.0f} s budget: "
+                      f"SURVEY §8(d)'s 100-query subset takes ~{100 * dt / done:.0f} s here; --cpu-search-budget "
+                      "raises it)",
             "rows": host16.shape[0], "k": k, "prep_s": round(t_prep, 2),
             "gpu_topk_matches_reference": f"{match}/{done}",
             "impl": "torch CPU fp32: index.float() / ||row|| once; per query q/||q||, q @ E^T, topk"}
+
+
+def _topk_ordered(s: torch.Tensor, i: torch.Tensor, k: int):
+    """top k of each row by (score desc, index asc): stable sort by index, then by score"""
+    o = torch.argsort(i, dim=1, stable=True)
+    s, i = torch.gather(s, 1, o), torch.gather(i, 1, o)
+    o = torch.argsort(-s, dim=1, stable=True)[:, :k]
+    return torch.gather(s, 1, o), torch.gather(i, 1, o)
 
 
 def search_leg(rows: int, queries: int, k: int, device, world: int = 1, rank: int = 0, keep_host: bool = False):
@@ -250,6 +265,7 @@ def search_leg(rows: int, queries: int, k: int, device, world: int = 1, rank: in
     top-k. The timed region spans local search + gather + merge, max over ranks.
     Every rank reports whether its shard built; all skip together if one failed (no rank is left
     waiting in a collective)."""
+    from clip_lora_match_amd import _capi as C
     from clip_lora_match_amd.distributed import shard_range
     from clip_lora_match_amd.search import CosineIndex
     dim = 512
@@ -257,25 +273,42 @@ def search_leg(rows: int, queries: int, k: int, device, world: int = 1, rank: in
     err = None
     idx = None
     host16 = None
+    nchk = min(32, queries)
+    chk_s = chk_i = None
     try:
         idx = CosineIndex(dim, capacity=max(stop - start, 1), device=device)
-        g = torch.Generator(device=device).manual_seed(7 + 1000 * rank)
-        if keep_host:
-            host16 = torch.empty((stop - start, dim), dtype=torch.float16)
-        chunk = 1 << 20
-        for r0 in range(start, stop, chunk):
-            n = min(chunk, stop - r0)
-            x = torch.randn((n, dim), generator=g, device=device)
-            xh = (x / x.norm(dim=-1, keepdim=True)).half()
-            idx.append(xh)
-            if host16 is not None:
-                host16[r0 - start: r0 - start + n] = xh.cpu()
-            del x, xh
         if world > 1:
             idx.set_offset(start)
-            g = torch.Generator(device=device).manual_seed(8)   # replicated queries
-        q = torch.randn((queries, dim), generator=g, device=device)
+        gq = torch.Generator(device=device).manual_seed(8)   # queries: replicated on every rank
+        q = torch.randn((queries, dim), generator=gq, device=device)
         q = (q / q.norm(dim=-1, keepdim=True)).half()
+        qchk = q[:nchk].float().contiguous()
+        if keep_host:
+            host16 = torch.empty((stop - start, dim), dtype=torch.float16)
+        # rows by GLOBAL position: chunk c = rows [c * 2^20, (c + 1) * 2^20) comes from seed 7 + c, so
+        # every world size searches the same index (each rank generates the chunks its shard overlaps)
+        chunk = 1 << 20
+        for c0 in range((start // chunk) * chunk, stop, chunk):
+            g = torch.Generator(device=device).manual_seed(7 + c0 // chunk)
+            x = torch.randn((min(chunk, rows - c0), dim), generator=g, device=device)
+            a, b = max(start, c0) - c0, min(stop, c0 + chunk) - c0
+            xh = (x[a:b] / x[a:b].norm(dim=-1, keepdim=True)).half()
+            del x
+            idx.append(xh)
+            if host16 is not None:
+                host16[c0 + a - start: c0 + b - start] = xh.cpu()
+            # independent check path: exact fp64 cosines (clm_cosine_scores) of the first queries
+            # against this piece, folded into a running top-k by (score desc, global index asc)
+            xf = xh.float().contiguous()
+            sc = torch.empty((nchk, xf.shape[0]), dtype=torch.float32, device=device)
+            C.check(C.lib().clm_cosine_scores(device.index, C.ptr(qchk), nchk, C.ptr(xf), xf.shape[0], dim, C.ptr(sc),
+                                              C.stream_of(device)), "clm_cosine_scores")
+            ts, ti = torch.topk(sc, min(k, xf.shape[0]), dim=1)
+            ti = ti + (c0 + a)
+            if chk_s is not None:
+                ts, ti = torch.cat([chk_s, ts], 1), torch.cat([chk_i, ti], 1)
+            chk_s, chk_i = _topk_ordered(ts, ti, k)
+            del xh, xf, sc
     except Exception as e:   # reported, never hidden
         err = repr(e)
     if world > 1:
@@ -310,11 +343,23 @@ def search_leg(rows: int, queries: int, k: int, device, world: int = 1, rank: in
         dt = float(t.item())
     st = idx.stats()
     idx.close()
+    # the check subset: gather every rank's exact top-k, order the union, compare with the fast path
+    if world > 1:
+        from clip_lora_match_amd.distributed import gather_candidates
+        chk_s, chk_i = gather_candidates(chk_s.contiguous(), chk_i.contiguous())
+    chk_s, chk_i = _topk_ordered(chk_s, chk_i, k)
+    match = int((torch.eq(chk_i, i[:nchk]).all(1) & torch.eq(chk_s, s[:nchk]).all(1)).sum())
+    import hashlib
     flops = 2.0 * queries * rows * dim
     out = {"qps": round(queries / dt, 1), "seconds": round(dt, 4), "rows": rows, "queries": queries, "k": k,
            "dim": dim, "index_dtype": "fp16", "tflops": round(flops / dt / 1e12, 1),
            "scores": "exact cosine (fp16 MFMA candidate pass + fp64 re-score), order (score desc, index asc)",
-           "paths": st}
+           "paths": st,
+           "check": {"queries": nchk, "match": f"{match}/{nchk}",
+                     "method": "first queries re-scored exactly (fp64 clm_cosine_scores) against every row, "
+                               "per-rank top-k gathered and ordered (score desc, index asc): indices and scores equal"},
+           "rows_seeded": "by global row (2^20-row chunks, seed 7 + chunk): the same index at every world size",
+           "topk_sha256": hashlib.sha256(i.cpu().numpy().tobytes()).hexdigest()[:16]}
     if world > 1:
         out.update({"n_gpus": world, "shard_rows": stop - start,
                     "parallelism": "row-sharded index, replicated queries, all_gather(top-k) + GPU merge"})
@@ -431,6 +476,129 @@ def parity_mode_leg(cfg, sd, lora, dev, B, imgs, ids, steps, warmup, lora_mode):
     m.close()
     return {"dtype": "fp16", "value": round(B / dt, 1), "unit": "image+text pairs/s", "ms_per_step": round(dt * 1e3, 4),
             "note": "fp16 operands, fp32 accumulate/residual/LN/softmax: scores within 1e-3 of the fp32 reference"}
+
+
+def parity_vs_golden(model, cfg, dev) -> dict:
+    """The timed model's error against the transformers fp32 goldens (tests/golden/enc_b32_lora_64.npz:
+    CLIPModel + LoRA hooks on 64 seeded 224^2 images + 64 full captions, B/32 synthetic weights),
+    computed outside the timed region: the max |score| error over the whole 128 x 128 matrix
+    (img.img, img.txt, txt.txt) and the max 1 - cos per embedding."""
+    g = np.load(os.path.join(REPO, "tests", "golden", "enc_b32_lora_64.npz"), allow_pickle=False)
+    imgs = torch.from_numpy(syn.images_u8(int(g["n_img"]), cfg.image_size, int(g["img_seed"]))).to(dev)
+    ids = torch.from_numpy(g["ids"]).to(dev)
+    a = torch.cat([model.encode_pixels(imgs), model.encode_ids(ids)]).double().cpu().numpy()
+    b = np.concatenate([g["emb_img"], g["emb_txt"]]).astype(np.float64)
+    cos = np.sum(a * b, 1) / (np.linalg.norm(a, axis=1) * np.linalg.norm(b, axis=1))
+    return {"max_score_err": float(np.abs(a @ a.T - b @ b.T).max()), "max_one_minus_cos": float(np.max(1 - cos)),
+            "bar": {"score": 1e-3, "source": "north_star: cosine scores within 1e-3"},
+            "reference": "transformers CLIPModel fp32 + LoRA hooks (tests/golden/enc_b32_lora_64.npz: 64 images + "
+                         "64 captions, B/32 + LoRA r=8)"}
+
+
+def lora_unmerged_leg(cfg, sd, lora, dev, B, imgs, ids, steps, warmup, dtype):
+    """The same step with the LoRA adapters kept unmerged (hot-swappable, models/clip_model.py:65-79):
+    the K-extension mode, Y = [X | X A^T] . [W | (alpha/r) B]^T, A's down-projection computed in the
+    LayerNorm kernel (q/k/v, fc1 inputs) or by lora_down (out_proj, fc2 inputs)."""
+    m = ClipLoraModel(cfg, device=dev, compute_dtype=dtype, lora_mode="unmerged", max_batch=B)
+    m.load_tensors(sd)
+    m.load_tensors(lora)
+    m.finalize()
+    oi = torch.empty((B, cfg.proj_dim), dtype=torch.float32, device=dev)
+    ot = torch.empty_like(oi)
+    for _ in range(warmup):
+        m.encode_pair(imgs, ids, out_img=oi, out_txt=ot, graph=True)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        m.encode_pair(imgs, ids, out_img=oi, out_txt=ot, graph=True)
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / steps
+    m.close()
+    return {"lora_mode": "unmerged (K-extension)", "value": round(B / dt, 1), "unit": "image+text pairs/s",
+            "ms_per_step": round(dt * 1e3, 4)}
+
+
+def index_build_leg(dev, world: int, rank: int, n_images: int, batch: int, dtype: str) -> dict:
+    """BASELINE configs[2] (scripts/rebuild_index.py:64-96 over images, batch-sharded): the product's
+    index_build.encode_items over n_images synthetic 224^2 images generated on the device batch by
+    batch (synthetic.DeviceImages: pixels a function of the global row, so every world size builds
+    the same index), B/32 + LoRA merged; rank r encodes shard_range(n, r, world) and one all_gather
+    (RCCL over xGMI at N > 1) gives every rank the index; rank 0 then writes the reference's .pt.
+    Timed end to end (max over ranks): generate + encode + re-normalise + all_gather, and the .pt
+    write. The all_gather alone is timed again afterwards on the same rows."""
+    import hashlib
+    import shutil
+    import tempfile
+    from clip_lora_match_amd.distributed import all_gather_rows, shard_range
+    from clip_lora_match_amd.index_build import _save_index, encode_items
+    from clip_lora_match_amd.processor import ClipProcessor
+    cfg = clm.get_preset("ViT-B/32")
+    m = ClipLoraModel(cfg, device=dev, compute_dtype=dtype, lora_mode="merged", max_batch=batch)
+    m.load_tensors(W.synthetic_state_dict(cfg, 0))
+    m.load_tensors(W.synthetic_lora(cfg, 1))
+    m.finalize()
+    proc = ClipProcessor(cfg)
+    src = syn.DeviceImages(n_images, cfg.image_size, seed=20240, device=dev)
+    m.encode_pixels(src.batch(0, min(batch, n_images)))   # untimed warm-up
+    names = [f"synthetic/{i:07d}.png" for i in range(n_images)]
+    texts = [""] * n_images
+
+    def sync():
+        torch.cuda.synchronize()
+        if world > 1:
+            torch.distributed.barrier()
+
+    def max_over_ranks(v: float) -> float:
+        if world == 1:
+            return v
+        t = torch.tensor([v], dtype=torch.float64, device=dev)
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        return float(t.item())
+
+    tmpdir = tempfile.mkdtemp(prefix="clm_index_") if rank == 0 else None
+    try:
+        sync()
+        t0 = time.perf_counter()
+        rows = encode_items(m, proc, images=src, batch_size=batch)
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        if rank == 0:
+            _save_index(rows.cpu(), texts, names, os.path.join(tmpdir, "index.pt"))
+        sync()
+        t2 = time.perf_counter()
+        enc_s, total_s = max_over_ranks(t1 - t0), max_over_ranks(t2 - t0)
+        gather_ms = None
+        if world > 1:
+            a, b = shard_range(n_images, rank, world)
+            local = rows[a:b].contiguous()
+            sync()
+            tg = time.perf_counter()
+            all_gather_rows(local, n_images)
+            torch.cuda.synchronize()
+            gather_ms = round(max_over_ranks(time.perf_counter() - tg) * 1e3, 3)
+        # checksum of checksums: a column-weighted fold of every row's bits, then sha256 of the folds
+        bits = rows.view(torch.int32).to(torch.int64)
+        fold = (bits * (torch.arange(bits.shape[1], device=dev, dtype=torch.int64) * 2 + 1)).sum(1)
+        sha = hashlib.sha256(fold.cpu().numpy().tobytes()).hexdigest()[:16]
+        pt_bytes = os.path.getsize(os.path.join(tmpdir, "index.pt")) if rank == 0 else None
+    finally:
+        m.close()
+        if tmpdir:
+            shutil.rmtree(tmpdir, ignore_errors=True)
+    flops = n_images * flops_per_pair(cfg, lora_merged=True)["image"]
+    out = {"config": "configs[2]: ViT-B/32 + LoRA r=8 index build over synthetic 224^2 images "
+                     "(index_build.encode_items + rank 0's .pt write)",
+           "images": n_images, "batch": batch, "dtype": "bf16" if dtype == "bfloat16" else "fp16",
+           "images_per_s": round(n_images / total_s, 1), "seconds": round(total_s, 3),
+           "encode_images_per_s": round(n_images / enc_s, 1), "encode_gather_s": round(enc_s, 3),
+           "write_s": round(total_s - enc_s, 3), "pt_bytes": pt_bytes,
+           "tflops": round(flops / enc_s / 1e12, 1), "index_fold_sha256": sha,
+           "note": "index_fold_sha256 is equal at every world size when the sharded build is bit-identical"}
+    if world > 1:
+        out.update({"n_gpus": world, "all_gather_ms": gather_ms,
+                    "all_gather_bytes": n_images * cfg.proj_dim * 4,
+                    "parallelism": "batch-sharded encode + all_gather(fp32 embeddings) over xGMI"})
+    return out
 
 
 def main():
@@ -565,6 +733,17 @@ def main():
             result["varlen_text"] = varlen_leg(model, cfg, dev, B, imgs, args.steps, args.warmup, rank)
         except Exception as e:  # report, never hide
             result["varlen_text"] = {"error": repr(e)}
+    if rank == 0:
+        try:
+            result["parity"] = {"dtype": result["dtype"], **parity_vs_golden(model, cfg, dev)}
+        except Exception as e:  # report, never hide
+            result["parity"] = {"error": repr(e)}
+    if rank == 0 and world == 1 and not args.no_unmerged and args.lora_mode == "merged":
+        try:
+            result["lora_unmerged"] = lora_unmerged_leg(cfg, sd, lora, dev, B, imgs, ids, args.steps, args.warmup,
+                                                        args.dtype)
+        except Exception as e:  # report, never hide
+            result["lora_unmerged"] = {"error": repr(e)}
     if rank == 0 and world == 1 and not args.no_parity_mode:
         try:
             result["parity_mode"] = parity_mode_leg(cfg, sd, lora, dev, B, imgs, ids, args.steps, args.warmup,
@@ -572,6 +751,13 @@ def main():
         except Exception as e:  # report, never hide
             result["parity_mode"] = {"error": repr(e)}
     model.close()
+    if not args.no_index_build:   # every rank takes part (batch-sharded + all_gather at N > 1)
+        try:
+            ib = index_build_leg(dev, world, rank, args.index_images, args.index_batch, args.dtype)
+        except Exception as e:  # report, never hide
+            ib = {"error": repr(e)}
+        if rank == 0:
+            result["index_build"] = ib
     host16 = qs_host = gpu_i = None
     if not args.no_search:   # every rank takes part when the index is sharded (world > 1)
         keep = rank == 0 and world == 1 and not args.no_cpu_baseline

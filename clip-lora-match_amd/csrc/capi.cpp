@@ -1269,10 +1269,15 @@ static int index_grow(clm_index* x, int64_t need_rows) {
   return CLM_OK;
 }
 
+// rescore_select / topk_merge order ties by a 32-bit image of the global row index
+constexpr int64_t MAX_GLOBAL_ROWS = (int64_t)0xFFFFFFFF;
+
 int clm_index_append(clm_index* x, const void* rows, int dtype, int64_t n, void* stream) {
   if (!x || n < 0 || (n > 0 && !rows)) return fail(CLM_E_ARG, "bad argument");
   if (dtype != CLM_F32 && dtype != CLM_F16) return fail(CLM_E_ARG, "rows must be f32 or f16");
   if (n == 0) return CLM_OK;
+  if (x->offset + x->n + n > MAX_GLOBAL_ROWS)
+    return fail(CLM_E_ARG, "index append: global row indices must stay below 2^32 (offset + rows)");
   DeviceGuard g(x->dev);
   hipStream_t st = (hipStream_t)stream;
   HIPCHK(hipStreamSynchronize(st));
@@ -1327,6 +1332,8 @@ int clm_index_reset(clm_index* x) {
 
 int clm_index_set_offset(clm_index* x, int64_t off) {
   if (!x || off < 0) return fail(CLM_E_ARG, "bad argument");
+  if (off + x->n > MAX_GLOBAL_ROWS)
+    return fail(CLM_E_ARG, "index offset: global row indices must stay below 2^32 (offset + rows)");
   x->offset = off;
   return CLM_OK;
 }
@@ -1533,11 +1540,35 @@ static int search_bounded(clm_index* x, bool sampled, int64_t S, const u16* q16,
   }
   x->search_stats[sampled ? 0 : 3] += nq - (int64_t)overflow.size();
   if (!overflow.empty()) {   // rare: a candidate list beyond CAND_CAP (many near-ties); redo exactly
+    // all overflowed queries of the call in ONE exact scan (the index is streamed once per query
+    // block of search_scan, not once per query): gather their fp32 rows and norms, scan, scatter
     x->search_stats[2] += (int64_t)overflow.size();
-    for (int64_t qi : overflow) {
-      r = search_scan(x, true, nullptr, nullptr, q32 + qi * dim, qn + qi, 1, k, osc + qi * k, oix + qi * k, st);
-      if (r) return r;
+    const int64_t no = (int64_t)overflow.size();
+    size_t o2 = 0;
+    auto take2 = [&](size_t bytes) { size_t o = o2; o2 = round_up(o2 + bytes, 256); return o; };
+    const size_t p_q = take2((size_t)no * dim * 4), p_n = take2((size_t)no * 8), p_s = take2((size_t)no * k * 4),
+                 p_i = take2((size_t)no * k * 8);
+    uint8_t* wo = nullptr;
+    if (hipMalloc(&wo, o2) != hipSuccess) { (void)hipGetLastError(); return fail(CLM_E_OOM, "overflow workspace"); }
+    float* gq = (float*)(wo + p_q);
+    double* gn = (double*)(wo + p_n);
+    float* gs = (float*)(wo + p_s);
+    int64_t* gi = (int64_t*)(wo + p_i);
+    hipError_t e = hipSuccess;
+    for (int64_t j = 0; j < no && e == hipSuccess; ++j) {
+      e = hipMemcpyAsync(gq + j * dim, q32 + overflow[j] * dim, (size_t)dim * 4, hipMemcpyDeviceToDevice, st);
+      if (e == hipSuccess) e = hipMemcpyAsync(gn + j, qn + overflow[j], 8, hipMemcpyDeviceToDevice, st);
     }
+    r = e == hipSuccess ? search_scan(x, true, nullptr, nullptr, gq, gn, no, k, gs, gi, st)
+                        : fail(CLM_E_HIP, std::string("overflow gather: ") + hipGetErrorString(e));
+    for (int64_t j = 0; j < no && r == CLM_OK && e == hipSuccess; ++j) {
+      e = hipMemcpyAsync(osc + overflow[j] * k, gs + j * k, (size_t)k * 4, hipMemcpyDeviceToDevice, st);
+      if (e == hipSuccess) e = hipMemcpyAsync(oix + overflow[j] * k, gi + j * k, (size_t)k * 8, hipMemcpyDeviceToDevice, st);
+    }
+    (void)hipStreamSynchronize(st);
+    (void)hipFree(wo);
+    if (r) return r;
+    if (e != hipSuccess) return fail(CLM_E_HIP, std::string("overflow scatter: ") + hipGetErrorString(e));
   }
   return CLM_OK;
 }
@@ -1882,5 +1913,16 @@ extern "C" int clm_resize_crop(int hip_device, const uint8_t* src, const int64_t
   if (e == hipSuccess) e = hipStreamSynchronize(st);
   (void)hipFree(w);
   if (e != hipSuccess) return fail(CLM_E_HIP, std::string("resize_crop: ") + hipGetErrorString(e));
+  return CLM_OK;
+}
+
+extern "C" int clm_synth_images(int hip_device, uint64_t seed, int64_t row0, int n, int S, uint8_t* out,
+                                void* stream) {
+  if (n < 0 || S <= 0 || row0 < 0 || ((int64_t)S * S * 3) % 16 || (n > 0 && !out))
+    return fail(CLM_E_ARG, "synth_images: bad argument (S * S * 3 must be a multiple of 16)");
+  if (n == 0) return CLM_OK;
+  if (!is_device_ptr(out) || ((uintptr_t)out & 15)) return fail(CLM_E_ARG, "synth_images: out must be 16-B aligned device memory");
+  DeviceGuard g(hip_device);
+  KCHK(synth_images(seed, row0, n, S, out, (hipStream_t)stream));
   return CLM_OK;
 }

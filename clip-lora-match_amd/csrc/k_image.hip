@@ -10,6 +10,8 @@
 // S kept rows need, then pass 2 for the S x S crop. Each output pixel depends only on its taps, so
 // the crop equals PIL's full resize followed by transformers' centre crop bit for bit.
 // Tap tables are built on the host (capi.cpp, double precision in PIL's operation order).
+#include <algorithm>
+
 #include "kernels.hpp"
 
 namespace clm {
@@ -80,7 +82,41 @@ __global__ __launch_bounds__(256) void resize_v_kernel(const uint8_t* __restrict
   o[2] = clip8(a2);
 }
 
+// Counter-based synthetic images (benchmarks / tests of the index build, BASELINE configs[2]):
+// byte b of image `row` is a function of (seed, row, b) only, so any shard of any batch split
+// regenerates the same pixels. 16 bytes per thread (two splitmix64 outputs), 16-B stores.
+__device__ __forceinline__ uint64_t splitmix64(uint64_t z) {
+  z += 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+__global__ __launch_bounds__(256) void synth_images_kernel(uint64_t seed, int64_t row0, int64_t per_image,
+                                                           int64_t total16, uint8_t* __restrict__ out) {
+  for (int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x; t < total16; t += (int64_t)gridDim.x * 256) {
+    const int64_t byte = t * 16;
+    const int64_t img = byte / per_image;
+    const uint64_t key = seed ^ ((uint64_t)(row0 + img) * 0xD1B54A32D192ED03ull);
+    const uint64_t w = (uint64_t)(byte - img * per_image) >> 3;
+    u32x4 v;
+    const uint64_t a = splitmix64(key + w), b = splitmix64(key + w + 1);
+    v.x = (uint32_t)a; v.y = (uint32_t)(a >> 32); v.z = (uint32_t)b; v.w = (uint32_t)(b >> 32);
+    *(u32x4*)(out + byte) = v;
+  }
+}
+
 }  // namespace
+
+hipError_t synth_images(uint64_t seed, int64_t row0, int n, int S, uint8_t* out, hipStream_t s) {
+  const int64_t per_image = (int64_t)S * S * 3;
+  if (n <= 0) return hipSuccess;
+  if (per_image % 16) return hipErrorInvalidValue;
+  const int64_t total16 = per_image * n / 16;
+  const unsigned blocks = (unsigned)std::min<int64_t>((total16 + 255) / 256, 8192);
+  synth_images_kernel<<<blocks, 256, 0, s>>>(seed, row0, per_image, total16, out);
+  return hipGetLastError();
+}
 
 hipError_t resize_crop(const uint8_t* src, const ResizeDesc* desc, int n, int S, int max_rows,
                        const int32_t* coef, uint8_t* tmp, uint8_t* out, hipStream_t s) {

@@ -118,6 +118,10 @@ struct ResizeDesc {
 hipError_t resize_crop(const uint8_t* src, const ResizeDesc* desc, int n, int S, int max_rows,
                        const int32_t* coef, uint8_t* tmp, uint8_t* out, hipStream_t s);
 
+// n synthetic uint8 [S, S, 3] images, image i's bytes a function of (seed, row0 + i) only
+// (S * S * 3 % 16 == 0; out 16-B aligned)
+hipError_t synth_images(uint64_t seed, int64_t row0, int n, int S, uint8_t* out, hipStream_t s);
+
 // patchify + (u8 rescale/normalise via lut | f32 copy) -> P[B*G*G, Kp] (compute dtype)
 hipError_t patchify(bool bf16, const void* pix, int layout, int B, int S, int p, int C,
                     const float* lut /*[C*256]*/, u16* P, int Kp, hipStream_t s);

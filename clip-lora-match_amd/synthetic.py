@@ -41,6 +41,32 @@ def odd_images(seed: int = 4242, sizes=ODD_SIZES) -> list:
     return out
 
 
+class DeviceImages:
+    """n synthetic uint8 [S, S, 3] images generated on the device batch by batch
+    (clm_synth_images): image i's pixels are a hash of (seed, i) only, so any shard / batch split
+    of the index build (BASELINE configs[2]) sees the same images. Sequence-like: len() and
+    batch(start, stop) -> uint8 device tensor [stop - start, S, S, 3]."""
+
+    def __init__(self, n: int, size: int, seed: int = 1234, device=None):
+        import torch
+        self.n, self.size, self.seed = int(n), int(size), int(seed)
+        self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+
+    def __len__(self) -> int:
+        return self.n
+
+    def batch(self, start: int, stop: int, out=None):
+        import torch
+        from . import _capi as C
+        start, stop = max(0, int(start)), min(self.n, int(stop))
+        n = max(stop - start, 0)
+        if out is None:
+            out = torch.empty((n, self.size, self.size, 3), dtype=torch.uint8, device=self.device)
+        C.check(C.lib().clm_synth_images(self.device.index, self.seed, start, n, self.size, C.ptr(out),
+                                         C.stream_of(self.device)), "clm_synth_images")
+        return out[:n]
+
+
 def captions(n: int, L: int, bos: int, eos: int, seed: int = 99, min_len: int = 8) -> np.ndarray:
     rng = np.random.Generator(np.random.PCG64(seed))
     ids = np.full((n, L), eos, np.int32)

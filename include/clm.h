@@ -120,6 +120,11 @@ int clm_encode_image(clm_ctx* ctx, const void* pixels, int pix_layout, int n, vo
 int clm_resize_crop(int hip_device, const uint8_t* src, const int64_t* offs, const int32_t* hw, int n,
                     int S, uint8_t* out, void* stream);
 
+/* Synthetic benchmark / test images (BASELINE configs[2]): out uint8 [n, S, S, 3] (device,
+ * 16-B aligned; S * S * 3 % 16 == 0) where every byte of image i is a hash of (seed, row0 + i,
+ * byte index) -- any shard / batch split of a global row range regenerates the same pixels. */
+int clm_synth_images(int hip_device, uint64_t seed, int64_t row0, int n, int S, uint8_t* out, void* stream);
+
 /* ids int32 [n, L] (L <= max_pos; each row holds an EOS) -> out [n, proj_dim] */
 int clm_encode_text(clm_ctx* ctx, const int32_t* ids, int n, int L, void* out, int out_dtype,
                     int normalize, void* stream);

@@ -56,8 +56,45 @@ def main(out_path, tmpdir):
     sh = ShardedIndex(dim, n)
     sh.append_shard(torch.from_numpy(rows[sh.start:sh.stop]))
     s_sh, i_sh = sh.search(torch.from_numpy(qs), k)
+    # 3. configs[2] in miniature: 64k device-generated images (seeded by global row), sharded build
+    #    through rebuild_index(from_images=True) with the .pt write; rank 0 redoes it unsharded with
+    #    another batch size (row results must not depend on the batch split)
+    n_big = 65_536
+    big = ClipLoraModel(cfg, compute_dtype="bfloat16", max_batch=256)
+    big.load_tensors(W.synthetic_state_dict(cfg, 0))
+    big.load_tensors(W.synthetic_lora(cfg, 1))
+    big.finalize()
+    src = syn.DeviceImages(n_big, cfg.image_size, seed=2024)
+    names = [f"synthetic/{i:06d}.png" for i in range(n_big)]
+    e_big = rebuild_index(big, proc, [""] * n_big, names, os.path.join(tmpdir, "big.pt"), batch_size=256,
+                          from_images=True, images=src)
+    big_file = torch.load(os.path.join(tmpdir, "big.pt"), map_location="cpu", weights_only=True)
+    # 4. a failed write on rank 0 raises on every rank (nobody is left in a collective)
+    blocker = os.path.join(tmpdir, "not_a_dir")
+    if rank == 0:
+        open(blocker, "w").close()
+    dist.barrier()
+    try:
+        rebuild_index(model, proc, caps[:4], ["a", "b", "c", "d"], os.path.join(blocker, "idx.pt"), batch_size=8)
+        raised = False
+    except RuntimeError as e:
+        raised = "rank 0 failed to write" in str(e) or rank == 0
+    except OSError:
+        raised = rank == 0   # rank 0 itself sees the OSError from mkdir
+    flag = torch.tensor([int(raised)])
+    dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+    res["write_failure_raised_everywhere"] = bool(flag.item())
     dist.barrier()
     if rank == 0:
+        ref_big = torch.cat([_renormalize(big.encode_pixels(src.batch(a, min(a + 200, n_big))))
+                             for a in range(0, n_big, 200)]).cpu()
+        res["big_build_equal"] = bool(torch.equal(e_big, ref_big))
+        res["big_file_equal"] = bool(torch.equal(big_file["embeddings"], ref_big))
+        res["big_file_rows"] = int(big_file["embeddings"].shape[0])
+        res["big_paths_ok"] = big_file["image_paths"][12345] == names[12345]
+        # the synthetic source is deterministic per global row, whatever the split
+        res["synth_rows_stable"] = bool(torch.equal(src.batch(1000, 1003).cpu(),
+                                                    torch.cat([src.batch(1000, 1001), src.batch(1001, 1003)]).cpu()))
         # single-rank references
         # (encode_items re-normalises each row once more, as rebuild_index.py:72 does)
         ref_img = torch.cat([_renormalize(model.encode_pixels(torch.from_numpy(np.stack(imgs[a:a + 8])).cuda()))
@@ -81,6 +118,7 @@ def main(out_path, tmpdir):
         res["merge_roundtrip"] = bool(torch.equal(i2, i1) and torch.equal(s2, s1))
         json.dump(res, open(out_path, "w"))
     dist.barrier()
+    big.close()
     model.close()
     dist.destroy_process_group()
 

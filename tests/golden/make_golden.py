@@ -201,11 +201,13 @@ def search_fp32_golden():
 
 
 if __name__ == "__main__":
-    which = sys.argv[1:] or ["tiny", "b32", "l14", "search", "search_fp32", "images"]
+    which = sys.argv[1:] or ["tiny", "b32", "b32_64", "l14", "search", "search_fp32", "images"]
     if "tiny" in which:
         encoder_golden("enc_tiny_lora.npz", "tiny", 4, 4, 16, True)
     if "b32" in which:
         encoder_golden("enc_b32_lora.npz", "ViT-B/32", 4, 4, 77, True)
+    if "b32_64" in which:   # the parity set bench.py scores its timed dtype against
+        encoder_golden("enc_b32_lora_64.npz", "ViT-B/32", 64, 64, 77, True, img_seed=5000, cap_seed=5001)
     if "l14" in which:
         encoder_golden("enc_l14_lora.npz", "ViT-L/14@336", 2, 2, 77, True)
     if "search" in which:

@@ -33,9 +33,11 @@ def test_sharded_build_and_search_world2(tmp_path):
     assert r["world"] == 2
     assert r["file_rows_min_max"] == [37, 37]     # both ranks read the complete file
     for key in ("build_img_equal", "build_txt_equal", "file_equal", "search_idx_equal", "search_scores_equal",
-                "merge_roundtrip"):
+                "merge_roundtrip", "big_build_equal", "big_file_equal", "big_paths_ok", "synth_rows_stable",
+                "write_failure_raised_everywhere"):
         assert r[key], (key, r)
     assert r["planted_top1"] == [5, 150_000, 150_001, 299_999]
+    assert r["big_file_rows"] == 65_536
 
 
 def test_bench_spawns_its_own_ranks(tmp_path):

@@ -296,6 +296,30 @@ def test_filtered_path_overflow_falls_back(monkeypatch):
     assert torch.all(s[0] > 0.999)
 
 
+def test_many_overflowing_queries_one_exact_rescan(monkeypatch):
+    """A block where most queries overflow their candidate lists (near-duplicate rows, like a
+    finder index built from one description template): they are redone together by one exact
+    scan and agree bit for bit with the full exact scan of every query."""
+    monkeypatch.setenv("CLM_SEARCH_BOUNDED", "1")
+    n, dim, k = 400_000, 128, 8
+    g = torch.Generator(device="cuda").manual_seed(5)
+    rows = torch.randn((n, dim), generator=g, device="cuda")
+    dups = torch.randn((3, dim), generator=g, device="cuda")
+    for j in range(3):   # three tie groups of 60k rows each
+        rows[j * 100_000: j * 100_000 + 60_000] = dups[j] + 1e-3 * torch.randn((60_000, dim), generator=g,
+                                                                                device="cuda")
+    idx = CosineIndex(dim, capacity=n)
+    idx.append(rows.half())
+    q = torch.cat([dups.repeat(20, 1), torch.randn((4, dim), generator=g, device="cuda")]).half()
+    s, i = idx.search(q, k)
+    assert idx.stats()["overflow"] >= 60
+    monkeypatch.delenv("CLM_SEARCH_BOUNDED")
+    monkeypatch.setenv("CLM_SEARCH_FULL", "1")
+    s_ref, i_ref = idx.search(q, k)
+    assert torch.equal(i, i_ref) and torch.equal(s, s_ref)
+    idx.close()
+
+
 # ---- query fusion (seeker_service.py:84-186) ------------------------------------------------
 def _unit_rows(n, d, seed):
     x = np.random.default_rng(seed).standard_normal((n, d)).astype(np.float32)
