@@ -1321,6 +1321,67 @@ int clm_index_append(clm_index* x, const void* rows, int dtype, int64_t n, void*
   return CLM_OK;
 }
 
+// Shard persistence (TextSearchIndex.save_shard / load_shard): the index's internal state as it
+// is, so a reload skips the fp32 normalisation and fp16 rounding of every row and searches bit for
+// bit as the index that was saved.
+int clm_index_has_f32(const clm_index* x) { return x ? (x->rows32 != nullptr) : -1; }
+
+static hipMemcpyKind copy_kind(const void* dst, const void* src) {
+  const bool d = is_device_ptr(dst), s = is_device_ptr(src);
+  return d ? (s ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice) : (s ? hipMemcpyDeviceToHost : hipMemcpyHostToHost);
+}
+
+int clm_index_export(clm_index* x, int64_t start, int64_t n, uint16_t* rows16, float* inv, float* rows32,
+                     void* stream) {
+  if (!x || start < 0 || n < 0 || start + n > x->n || (n > 0 && (!rows16 || !inv)))
+    return fail(CLM_E_ARG, "index export: bad range or null destination");
+  if (rows32 && !x->rows32) return fail(CLM_E_STATE, "index export: the index keeps no fp32 rows");
+  if (n == 0) return CLM_OK;
+  DeviceGuard g(x->dev);
+  hipStream_t st = (hipStream_t)stream;
+  const size_t cnt = (size_t)n * x->dim;
+  HIPCHK(hipMemcpyAsync(rows16, x->rows + (size_t)start * x->dim, cnt * 2, copy_kind(rows16, x->rows), st));
+  HIPCHK(hipMemcpyAsync(inv, x->inv + start, (size_t)n * 4, copy_kind(inv, x->inv), st));
+  if (rows32)
+    HIPCHK(hipMemcpyAsync(rows32, x->rows32 + (size_t)start * x->dim, cnt * 4, copy_kind(rows32, x->rows32), st));
+  HIPCHK(hipStreamSynchronize(st));
+  return CLM_OK;
+}
+
+int clm_index_import(clm_index* x, const uint16_t* rows16, const float* inv, const float* rows32, int64_t n,
+                     void* stream) {
+  if (!x || n < 0 || (n > 0 && (!rows16 || !inv))) return fail(CLM_E_ARG, "index import: bad argument");
+  if (n == 0) return CLM_OK;
+  if (x->offset + x->n + n > MAX_GLOBAL_ROWS)
+    return fail(CLM_E_ARG, "index import: global row indices must stay below 2^32 (offset + rows)");
+  DeviceGuard g(x->dev);
+  hipStream_t st = (hipStream_t)stream;
+  HIPCHK(hipStreamSynchronize(st));
+  int r = index_grow(x, x->n + n);
+  if (r) return r;
+  x->samp_n = -1;
+  const size_t cnt = (size_t)n * x->dim;
+  if (rows32 && !x->rows32) {   // as clm_index_append: the first fp32 rows start the fp32 copy
+    if (hipMalloc(&x->rows32, (size_t)x->cap * x->dim * sizeof(float)) != hipSuccess) {
+      (void)hipGetLastError();
+      x->rows32 = nullptr;
+      return fail(CLM_E_OOM, "fp32 row copy allocation failed");
+    }
+    KCHK(f16_to_f32_rows(x->rows, x->n, (int)x->dim, x->rows32, st));
+  }
+  u16* d16 = x->rows + (size_t)x->n * x->dim;
+  HIPCHK(hipMemcpyAsync(d16, rows16, cnt * 2, copy_kind(d16, rows16), st));
+  HIPCHK(hipMemcpyAsync(x->inv + x->n, inv, (size_t)n * 4, copy_kind(x->inv, inv), st));
+  if (x->rows32) {
+    float* d32 = x->rows32 + (size_t)x->n * x->dim;
+    if (rows32) HIPCHK(hipMemcpyAsync(d32, rows32, cnt * 4, copy_kind(d32, rows32), st));
+    else KCHK(f16_to_f32_rows(d16, n, (int)x->dim, d32, st));   // fp16 rows are the caller's rows
+  }
+  HIPCHK(hipStreamSynchronize(st));
+  x->n += n;
+  return CLM_OK;
+}
+
 int64_t clm_index_size(const clm_index* x) { return x ? x->n : -1; }
 
 int clm_index_reset(clm_index* x) {

@@ -76,6 +76,14 @@ class FinderIndex:
         locations = list(locations) if locations is not None else [None] * n
         reporters = list(reporters) if reporters is not None else [None] * n
         found_at = list(found_at) if found_at is not None else [None] * n
+        # checked before any image is copied: token-id descriptions have no text to append a
+        # location to (finder_service.py:123-131 builds "<description>, ditemukan di <location>"),
+        # and one batch is either all strings or all token ids
+        is_str = [isinstance(d, str) for d in descriptions]
+        if any(is_str) and not all(is_str):
+            raise ValueError("descriptions must be all strings or all token-id lists, not a mix")
+        if not all(is_str) and any(loc for loc in locations):
+            raise ValueError("a location needs a string description (token ids cannot carry it)")
         rel_paths = [self._store_image(p) for p in src_image_paths]
         texts = []
         for d, loc in zip(descriptions, locations):

@@ -9,7 +9,11 @@ exact top-k kernels.
 New: .append / .save keep the index resident with amortised
 O(1) append instead of FinderService's torch.cat + full re-save per report
 (finder_service.py:93-103,172-185; the report flow itself is finder.py), and
-.search_batch serves many queries per launch.
+.search_batch serves many queries per launch. .save_shard / .load_shard persist the HBM
+index itself (SURVEY §5 checkpoint row): a raw shard of the fp16 MFMA operands, their fp32
+inverse norms and the fp32 rows, streamed back to HBM without re-normalising or re-rounding
+anything (the .pt reload of search.py:29-36,68 costs torch.load + an fp32 normalise of every
+row + the fp16 rounding), bit-identical in search.
 
 Scores are the exact cosines of the stored fp32 rows (fp64 arithmetic, rounded
 once): the fp16 MFMA pass only bounds the candidates (clm_index_search). Top-k
@@ -19,6 +23,8 @@ order (SURVEY §7 hard part 2).
 from __future__ import annotations
 
 import ctypes
+import json
+import struct
 from dataclasses import dataclass
 from pathlib import Path
 from typing import List, Optional, Sequence, Tuple, Union
@@ -104,6 +110,74 @@ class CosineIndex:
                                          C.stream_of(self.device)), "clm_index_search")
         return s, i
 
+    # ------------------------------------------------------------ shard file --
+    def save_shard(self, path: Union[str, Path], meta: Optional[dict] = None, chunk_rows: int = 1 << 20) -> None:
+        """Write the index's internal state (fp16 operands, fp32 inverse norms, the fp32 rows if
+        kept) to a shard file (format: _SHARD_MAGIC, u64 header length, JSON header, then the
+        sections at 4 KiB boundaries), streamed through a pinned host buffer; atomic rename."""
+        path = Path(path)
+        path.parent.mkdir(parents=True, exist_ok=True)
+        n = len(self)
+        has32 = int(C.lib().clm_index_has_f32(self._h)) == 1
+        header = {"format": "clm-index-shard", "version": 1, "dim": self.dim, "dim_p": self.dim_p, "n": n,
+                  "has_f32": has32, "meta": meta or {}}
+        hb = json.dumps(header).encode()
+        tmp = path.with_name(path.name + ".tmp")
+        chunk = max(1, min(int(chunk_rows), max(n, 1)))
+        b16 = torch.empty((chunk, self.dim_p), dtype=torch.float16, pin_memory=True)
+        binv = torch.empty((chunk,), dtype=torch.float32, pin_memory=True)
+        b32 = torch.empty((chunk, self.dim_p), dtype=torch.float32, pin_memory=True) if has32 else None
+        secs = _shard_sections(len(hb), n, self.dim_p, has32)
+        with open(tmp, "wb") as f:
+            f.write(_SHARD_MAGIC + struct.pack("<Q", len(hb)) + hb)
+            for r0 in range(0, n, chunk):
+                m = min(chunk, n - r0)
+                C.check(C.lib().clm_index_export(self._h, r0, m, C.ptr(b16), C.ptr(binv),
+                                                 C.ptr(b32) if b32 is not None else None,
+                                                 C.stream_of(self.device)), "clm_index_export")
+                for name, buf in (("rows16", b16), ("inv", binv), ("rows32", b32)):
+                    if buf is None:
+                        continue
+                    f.seek(secs[name][0] + r0 * buf[0].numel() * buf.element_size())
+                    f.write(memoryview(buf[:m].numpy()).cast("B"))
+            f.truncate(_shard_size(secs))
+        tmp.replace(path)
+
+    @classmethod
+    def load_shard(cls, path: Union[str, Path], device=None, capacity: Optional[int] = None,
+                   chunk_rows: int = 1 << 20) -> Tuple["CosineIndex", dict]:
+        """(index, header) from a shard file: the sections are read chunk by chunk into a pinned
+        buffer and imported into HBM as they are (clm_index_import)."""
+        path = Path(path)
+        if not path.exists():
+            raise FileNotFoundError(f"Index shard not found: {path}")
+        header, secs = read_shard_header(path)
+        n, dim_p = header["n"], header["dim_p"]
+        idx = cls(header["dim"], capacity=max(capacity or n, 1), device=device)
+        if idx.dim_p != dim_p:
+            raise ValueError(f"shard dim_p {dim_p} does not match dim {header['dim']}")
+        chunk = max(1, min(int(chunk_rows), max(n, 1)))
+        b16 = torch.empty((chunk, dim_p), dtype=torch.float16, pin_memory=True)
+        binv = torch.empty((chunk,), dtype=torch.float32, pin_memory=True)
+        b32 = torch.empty((chunk, dim_p), dtype=torch.float32, pin_memory=True) if header["has_f32"] else None
+        with open(path, "rb", buffering=0) as f:
+            for r0 in range(0, n, chunk):
+                m = min(chunk, n - r0)
+                for name, buf in (("rows16", b16), ("inv", binv), ("rows32", b32)):
+                    if buf is None:
+                        continue
+                    row_bytes = buf[0].numel() * buf.element_size()
+                    f.seek(secs[name][0] + r0 * row_bytes)
+                    view = memoryview(buf.numpy()).cast("B")[: m * row_bytes]
+                    if f.readinto(view) != m * row_bytes:
+                        raise ValueError(f"truncated index shard {path} (section {name})")
+                d16 = b16[:m].to(idx.device, non_blocking=True)
+                dinv = binv[:m].to(idx.device, non_blocking=True)
+                d32 = b32[:m].to(idx.device, non_blocking=True) if b32 is not None else None
+                C.check(C.lib().clm_index_import(idx._h, C.ptr(d16), C.ptr(dinv), C.ptr(d32) if d32 is not None else None,
+                                                 m, C.stream_of(idx.device)), "clm_index_import")
+        return idx, header
+
     def stats(self) -> dict:
         """queries served by the sampled single-pass bounded search (`filtered`), the bounded
         search with a chunked fp16 scan as its first step (`scan_bounded`), the full exact
@@ -123,6 +197,42 @@ class CosineIndex:
             self.close()
         except Exception:
             pass
+
+
+_SHARD_MAGIC = b"CLMIDX01"
+
+
+def _shard_sections(header_len: int, n: int, dim_p: int, has32: bool) -> dict:
+    """byte offset and length of each section, every one at a 4 KiB boundary"""
+    def up(x):
+        return (x + 4095) // 4096 * 4096
+    off = up(len(_SHARD_MAGIC) + 8 + header_len)
+    secs = {}
+    for name, nbytes in (("rows16", n * dim_p * 2), ("inv", n * 4), ("rows32", n * dim_p * 4 if has32 else 0)):
+        if nbytes or name != "rows32":
+            secs[name] = (off, nbytes)
+            off = up(off + nbytes)
+    return secs
+
+
+def _shard_size(secs: dict) -> int:
+    return max(o + b for o, b in secs.values())
+
+
+def read_shard_header(path: Union[str, Path]) -> Tuple[dict, dict]:
+    """(header, sections) of a shard file; ValueError if it is not one"""
+    with open(path, "rb") as f:
+        magic = f.read(len(_SHARD_MAGIC))
+        if magic != _SHARD_MAGIC:
+            raise ValueError(f"{path} is not a clm index shard")
+        (hl,) = struct.unpack("<Q", f.read(8))
+        header = json.loads(f.read(hl).decode())
+    if header.get("format") != "clm-index-shard" or header.get("version") != 1:
+        raise ValueError(f"{path}: unsupported shard header {header.get('format')} v{header.get('version')}")
+    secs = _shard_sections(hl, header["n"], header["dim_p"], header["has_f32"])
+    if Path(path).stat().st_size < _shard_size(secs):
+        raise ValueError(f"truncated index shard {path}")
+    return header, secs
 
 
 class TextSearchIndex:
@@ -254,3 +364,36 @@ class TextSearchIndex:
         torch.save({"embeddings": self.embeddings.clone(), "image_paths": list(self.image_paths),
                     "texts": list(self.texts)}, tmp)
         tmp.replace(path)
+
+    # ------------------------------------------------------------ shard file --
+    def save_shard(self, path: Union[str, Path]) -> None:
+        """The HBM index as a raw shard (CosineIndex.save_shard) with this index's metadata; the
+        reference .pt stays available through .save."""
+        self._gpu.save_shard(path, meta={"image_paths": [str(p) for p in self.image_paths],
+                                         "texts": [str(t) for t in self.texts]})
+
+    @classmethod
+    def load_shard(cls, path: Union[str, Path], device=None) -> "TextSearchIndex":
+        """Reload a save_shard file straight into HBM (no torch.load, no re-normalisation): the
+        same rows, metadata and search results, bit for bit, as the index that was saved."""
+        gpu, header = CosineIndex.load_shard(path, device=device, capacity=max(header_n(path), 1024))
+        self = cls.__new__(cls)
+        n, dim, dim_p = header["n"], header["dim"], header["dim_p"]
+        _, secs = read_shard_header(path)
+        if header["has_f32"]:   # the host mirror: the fp32 rows, paged in lazily (copy-on-write map)
+            host = np.memmap(path, dtype=np.float32, mode="c", offset=secs["rows32"][0], shape=(n, dim_p))
+        else:
+            host = np.memmap(path, dtype=np.float16, mode="r", offset=secs["rows16"][0], shape=(n, dim_p))
+        host = torch.from_numpy(np.ascontiguousarray(host[:, :dim]) if dim != dim_p or not header["has_f32"]
+                                else host).float()
+        self._host, self._n = host, n
+        self.image_paths = list(header["meta"].get("image_paths", []))
+        self.texts = list(header["meta"].get("texts", []))
+        self.num_items, self.dim = n, dim
+        self._gpu = gpu
+        print(f"[TextSearchIndex] Loaded {n} items with dim={dim} (shard)")
+        return self
+
+
+def header_n(path) -> int:
+    return read_shard_header(path)[0]["n"]

@@ -24,6 +24,8 @@
  *   clm_topk_merge             (new) merge of per-shard top-k lists for the
  *                              8-GPU sharded search
  *   clm_l2_normalize           v / ||v||_2 (clip_model.py:116,148; search.py:68,93)
+ *   clm_index_export/_import   the index's .pt persistence (search.py:29-36,68;
+ *                              finder_service.py:93-103) as a raw fp16 shard
  *   clm_resize_crop            CLIPProcessor's image resize + centre crop for inputs of any
  *                              size (clip_model.py:105-110, embed_image.py:36-41;
  *                              config/clip_config.yaml:7-9)
@@ -156,6 +158,18 @@ int clm_index_reset(clm_index* idx);
 int clm_index_set_offset(clm_index* idx, int64_t global_offset);
 /* copy rows [start, start+n) back as fp32 (host or device dst) */
 int clm_index_read(clm_index* idx, int64_t start, int64_t n, float* dst, void* stream);
+/* Shard persistence (TextSearchIndex.save_shard / load_shard; the reference persists its index
+ * as a .pt, search.py:29-36 / finder_service.py:93-103): export copies rows [start, start+n) of
+ * the index's internal state -- fp16 MFMA operands rows16 [n, dim], their fp32 inverse norms
+ * inv [n] and, when rows32 != NULL, the fp32 rows the index keeps (CLM_E_STATE if it keeps none;
+ * clm_index_has_f32 says) -- to host or device memory. import appends n rows in exactly that
+ * form (no normalisation or rounding), so the reloaded index searches bit for bit as the saved
+ * one. Both synchronous. */
+int clm_index_has_f32(const clm_index* idx);
+int clm_index_export(clm_index* idx, int64_t start, int64_t n, uint16_t* rows16, float* inv, float* rows32,
+                     void* stream);
+int clm_index_import(clm_index* idx, const uint16_t* rows16, const float* inv, const float* rows32, int64_t n,
+                     void* stream);
 /* q [nq, dim] CLM_F32|CLM_F16 (normalised in-kernel); k in [1, 1024];
  * out_scores [nq, k] f32 = exact cosines, out_idx [nq, k] i64 (+ global offset);
  * order: score desc, index asc (CPU torch.topk, search.py:98-99, leaves ties unordered);

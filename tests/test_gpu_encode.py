@@ -2,11 +2,12 @@
 the transformers-generated goldens.
 
 Tolerances (written here, derived in DESIGN.md §Numerics):
-  * fp16 operands (parity mode): cosine-score matrices (img.img, img.txt, txt.txt)
-    within 1e-3 of the fp32 reference -- the north_star bar; embedding cosine
-    distance 1 - cos(gpu, ref) <= 1e-5.
-  * bf16 operands (throughput mode, BASELINE config 1): 8 fewer mantissa bits
-    in every GEMM operand; scores within 4e-3, 1 - cos <= 1e-4.
+  * fp16 operands (the default and the bench headline): cosine-score matrices (img.img,
+    img.txt, txt.txt) within 1e-3 of the fp32 reference -- the north_star bar; embedding
+    cosine distance 1 - cos(gpu, ref) <= 1e-5.
+  * bf16 operands (BASELINE config 1's wording): 3 fewer mantissa bits in every GEMM
+    operand; measured max score error 1.7e-3 on the 64 + 64 parity set (over the 1e-3 bar,
+    which is why fp16 is the headline), bar 2.5e-3, 1 - cos <= 1e-4.
 """
 import numpy as np
 import pytest
@@ -19,7 +20,7 @@ from clip_lora_match_amd import synthetic as syn
 from clip_lora_match_amd.engine import ClipLoraModel
 from oracle import clip_ref as R
 
-TOL = {"float16": dict(score=1e-3, cos=1e-5), "bfloat16": dict(score=4e-3, cos=1e-4)}
+TOL = {"float16": dict(score=1e-3, cos=1e-5), "bfloat16": dict(score=2.5e-3, cos=1e-4)}
 
 pytestmark = pytest.mark.gpu
 
@@ -66,6 +67,23 @@ def test_b32_lora_golden(dtype):
     _check(gi, gt, g["emb_img"], g["emb_txt"], dtype)
     # LoRA must matter far beyond the tolerance (non-vacuous parity)
     assert np.max(np.abs(g["emb_txt"] - g["emb_txt_base"])) > 10 * TOL[dtype]["score"]
+
+
+@pytest.mark.parametrize("dtype", ["float16", "bfloat16"])
+def test_b32_lora_parity_set_64(dtype):
+    """the 64 images + 64 captions bench.py's `parity` object scores (whole 128 x 128 score
+    matrix); prints the measured errors"""
+    g = golden("enc_b32_lora_64.npz")
+    m, cfg, sd, lora = _model("ViT-B/32", dtype, max_batch=64)
+    imgs = syn.images_u8(int(g["n_img"]), cfg.image_size, int(g["img_seed"]))
+    a = np.concatenate([m.encode_pixels(torch.from_numpy(imgs).cuda()).cpu().numpy(),
+                        m.encode_ids(torch.from_numpy(g["ids"]).cuda()).cpu().numpy()]).astype(np.float64)
+    b = np.concatenate([g["emb_img"], g["emb_txt"]]).astype(np.float64)
+    err = np.max(np.abs(a @ a.T - b @ b.T))
+    cos = np.max(1 - np.sum(a * b, 1) / (np.linalg.norm(a, axis=1) * np.linalg.norm(b, axis=1)))
+    print(f"\nB/32 + LoRA {dtype}: max score err {err:.3e}, max 1 - cos {cos:.3e}")
+    assert err <= TOL[dtype]["score"] and cos <= TOL[dtype]["cos"], (err, cos)
+    m.close()
 
 
 def test_b32_unmerged_matches_merged():

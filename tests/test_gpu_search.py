@@ -480,3 +480,60 @@ class _sparse_scores:
 
     def __getitem__(self, idx):
         return np.array([self.d.get(int(t), -9.0) for t in np.atleast_1d(idx)])
+
+
+# ---- shard persistence (SURVEY §5 checkpoint row) ---------------------------------------------
+def test_shard_roundtrip_bit_identical_to_pt_reload(tmp_path):
+    """TextSearchIndex.save_shard / load_shard vs the reference .pt reload of the same index:
+    same rows, metadata and search results bit for bit; appends keep working after a reload."""
+    from clip_lora_match_amd.search import TextSearchIndex, read_shard_header
+    rows = syn.clustered_rows(300, 40, 512, 0.05, seed=71)           # 12,000 fp32 rows, near-ties
+    q = torch.from_numpy(syn.clustered_rows(300, 1, 512, 0.05, seed=71, noise_seed=72)[:64])
+    pt = tmp_path / "idx.pt"
+    torch.save({"embeddings": torch.from_numpy(rows), "image_paths": [f"p{i}.jpg" for i in range(len(rows))],
+                "texts": [f"t{i}" for i in range(len(rows))]}, pt)
+    a = TextSearchIndex(pt)
+    shard = tmp_path / "idx.clmidx"
+    a.save_shard(shard)
+    hdr, secs = read_shard_header(shard)
+    assert hdr["n"] == len(rows) and hdr["has_f32"] and all(o % 4096 == 0 for o, _ in secs.values())
+    b = TextSearchIndex.load_shard(shard)
+    assert b.num_items == a.num_items and b.dim == 512
+    assert torch.equal(b.embeddings, a.embeddings)
+    assert b.image_paths == a.image_paths and b.texts == a.texts
+    for k in (1, 5, 50):
+        sa, ia = a.search_batch(q, k)
+        sb, ib = b.search_batch(q, k)
+        assert torch.equal(ia, ib) and torch.equal(sa, sb)
+    r = b.search_with_embedding(q[3], top_k=3)
+    assert r[0].image_path == f"p{r[0].index}.jpg" and r[0].text == f"t{r[0].index}"
+    extra = torch.from_numpy(syn.gaussian_rows(10, 512, 73, fp16=False))
+    a.append(extra, [f"x{i}" for i in range(10)], [""] * 10)
+    b.append(extra, [f"x{i}" for i in range(10)], [""] * 10)
+    sa, ia = a.search_batch(extra[:4], 2)
+    sb, ib = b.search_batch(extra[:4], 2)
+    assert torch.equal(ia, ib) and torch.equal(sa, sb) and ia[:, 0].tolist() == list(range(12000, 12004))
+
+
+def test_fp16_shard_roundtrip_and_bad_files(tmp_path):
+    """An fp16 CosineIndex (no fp32 copy, the configs[4] layout) in small chunks; a file that is
+    not a shard raises ValueError, a missing one FileNotFoundError."""
+    rows = torch.from_numpy(syn.gaussian_rows(5000, 256, 74, fp16=True))
+    idx = CosineIndex(256)
+    idx.append(rows)
+    p = tmp_path / "f16.clmidx"
+    idx.save_shard(p, chunk_rows=777)
+    re_, hdr = CosineIndex.load_shard(p, chunk_rows=1000)
+    assert not hdr["has_f32"] and len(re_) == 5000
+    q = rows[:32].float() + 0.01
+    s1, i1 = idx.search(q, 7)
+    s2, i2 = re_.search(q, 7)
+    assert torch.equal(i1, i2) and torch.equal(s1, s2)
+    bad = tmp_path / "bad.clmidx"
+    bad.write_bytes(b"not a shard at all")
+    with pytest.raises(ValueError):
+        CosineIndex.load_shard(bad)
+    with pytest.raises(FileNotFoundError):
+        CosineIndex.load_shard(tmp_path / "missing.clmidx")
+    idx.close()
+    re_.close()
