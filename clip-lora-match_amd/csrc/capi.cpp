@@ -103,10 +103,6 @@ struct LayerW {
   u16* w_out = nullptr; float* b_out = nullptr; int k_out = 0;
   u16* w_fc1 = nullptr; float* b_fc1 = nullptr; int k_fc1 = 0;
   u16* w_fc2 = nullptr; float* b_fc2 = nullptr; int k_fc2 = 0;
-  // LayerNorm folded into the following GEMM (ln_fold): W' = W diag(gamma) (16-bit), bias' =
-  // b + W beta, c = row sums of the rounded W' -- for qkv (LN1, layers >= 1) and fc1 (LN2)
-  u16* w_qkv_f = nullptr; float* b_qkv_f = nullptr; float* c_qkv = nullptr;
-  u16* w_fc1_f = nullptr; float* b_fc1_f = nullptr; float* c_fc1 = nullptr;
   float* a_qkv = nullptr; int r_qkv = 0;   // unmerged LoRA A (fp32) per GEMM input
   float* a_out = nullptr; int r_out = 0;
   float* a_fc1 = nullptr; int r_fc1 = 0;
@@ -128,8 +124,6 @@ struct Tower {
   float* h = nullptr;
   u16 *X = nullptr, *QKV = nullptr, *O = nullptr, *Hm = nullptr, *P = nullptr;
   float* pooled = nullptr;  // [max_batch, proj_dim] un-normalised projections
-  float2* stats = nullptr; // [maxM, d / 32] per-row 32-column moments of the residual GEMMs (ln_fold)
-  float2* lnst = nullptr;   // [maxM] (rstd, -rstd * mean) of the pending LayerNorm (ln_fold)
   float* hc = nullptr;      // [max_batch, d] pooled residual rows of the pruned last layer
   u16* Oc = nullptr;        // [max_batch, ldo] their attention-output rows
   // varlen text plan (text_plan): per caption live rows / offsets, packed-row map, fused-attention
@@ -147,7 +141,6 @@ struct clm_ctx {
   clm_model_desc desc{};
   bool finalized = false;
   bool lora_enabled = true;
-  bool ln_fold = false;   // LayerNorm folded into qkv / fc1 (merged LoRA; opt-in $CLM_LN_FOLD=1)
   std::unordered_map<std::string, HostTensor> host;
   std::vector<void*> allocs;       // weights + workspace
   Tower vis, txt;
@@ -347,33 +340,6 @@ int build_fused(clm_ctx* c, const std::vector<LinearSpec>& specs, bool q_scale_f
   return CLM_OK;
 }
 
-float round16(bool bf, float v) { return bf ? host_bf16_to_f32(host_f32_to_bf16(v)) : host_f16_to_f32(host_f32_to_f16(v)); }
-
-// Linear(LayerNorm(h)) = rstd * (h W'^T) - rstd * mean * c + bias' with W' = W diag(gamma),
-// c[o] = sum_k W'16[o, k] (the rounded operand the GEMM uses, so the mean term cancels against
-// it exactly), bias'[o] = bias[o] + sum_k W[o, k] beta[k] (fp64 sums of the fp32 weights).
-int fold_ln(clm_ctx* c, const std::vector<float>& W, const std::vector<float>& bias, int out, int K,
-            const std::string& ln, u16** w_dst, float** b_dst, float** c_dst) {
-  const HostTensor *g, *b;
-  int r;
-  if ((r = need(c, ln + ".weight", K, &g)) || (r = need(c, ln + ".bias", K, &b))) return r;
-  std::vector<float> Wf((size_t)out * K), bf(out), cs(out);
-  for (int o = 0; o < out; ++o) {
-    double sc = 0.0, sb = bias[o];
-    for (int k = 0; k < K; ++k) {
-      const float w = W[(size_t)o * K + k];
-      const float wf = w * g->data[k];
-      Wf[(size_t)o * K + k] = wf;
-      sc += round16(c->bf16(), wf);
-      sb += (double)w * b->data[k];
-    }
-    cs[o] = (float)sc;
-    bf[o] = (float)sb;
-  }
-  if ((r = upload_16(c, Wf, w_dst)) || (r = upload_f32(c, bf, b_dst)) || (r = upload_f32(c, cs, c_dst))) return r;
-  return CLM_OK;
-}
-
 int build_tower(clm_ctx* c, Tower& T, bool vision) {
   const clm_model_desc& d = c->desc;
   const clm_tower_desc& td = vision ? d.vision : d.text;
@@ -403,9 +369,6 @@ int build_tower(clm_ctx* c, Tower& T, bool vision) {
     if ((r = build_fused(c, qkv, true, W, b, K, A, rext))) return r;
     if ((r = upload_16(c, W, &Lw.w_qkv)) || (r = upload_f32(c, b, &Lw.b_qkv))) return r;
     Lw.k_qkv = K; Lw.r_qkv = rext;
-    if (c->ln_fold && l > 0 &&
-        (r = fold_ln(c, W, b, 3 * T.d, K, p + ".layer_norm1", &Lw.w_qkv_f, &Lw.b_qkv_f, &Lw.c_qkv)))
-      return r;
     if (unmerged && rext && (r = upload_f32(c, A, &Lw.a_qkv))) return r;
 
     std::vector<LinearSpec> outp = {{p + ".self_attn.out_proj", T.d, T.d, (tg & CLM_LORA_OUT) != 0}};
@@ -418,8 +381,6 @@ int build_tower(clm_ctx* c, Tower& T, bool vision) {
     if ((r = build_fused(c, fc1, false, W, b, K, A, rext))) return r;
     if ((r = upload_16(c, W, &Lw.w_fc1)) || (r = upload_f32(c, b, &Lw.b_fc1))) return r;
     Lw.k_fc1 = K; Lw.r_fc1 = rext;
-    if (c->ln_fold && (r = fold_ln(c, W, b, T.mlp, K, p + ".layer_norm2", &Lw.w_fc1_f, &Lw.b_fc1_f, &Lw.c_fc1)))
-      return r;
     if (unmerged && rext && (r = upload_f32(c, A, &Lw.a_fc1))) return r;
 
     std::vector<LinearSpec> fc2 = {{p + ".mlp.fc2", T.mlp, T.d, (tg & CLM_LORA_FC2) != 0}};
@@ -480,10 +441,6 @@ int build_tower(clm_ctx* c, Tower& T, bool vision) {
   if ((r = c->dalloc(&T.O, (size_t)T.maxM * T.ldo))) return r;
   if ((r = c->dalloc(&T.Hm, (size_t)T.maxM * T.ldm))) return r;
   if ((r = c->dalloc(&T.pooled, (size_t)B * d.proj_dim))) return r;
-  if (c->ln_fold) {
-    if ((r = c->dalloc(&T.stats, (size_t)T.maxM * (T.d / 32)))) return r;
-    if ((r = c->dalloc(&T.lnst, (size_t)T.maxM))) return r;
-  }
   if ((r = c->dalloc(&T.hc, (size_t)B * T.d))) return r;
   if ((r = c->dalloc(&T.Oc, (size_t)B * T.ldo))) return r;
   if (!T.vision) {
@@ -571,7 +528,7 @@ bool prune_last_layer() {
 // output. Only each caption's live rows (through its first EOS) are packed and encoded; the
 // embeddings are bit-identical to encoding all L rows (rows are independent in every kernel but
 // attention, whose keys of a live query are all live; tests/test_gpu_encode.py). Needs the fused
-// attention kernel, no LayerNorm folding and no unmerged-LoRA K-extension.
+// attention kernel and no unmerged-LoRA K-extension.
 bool text_varlen_enabled() {
   static int v = -1;
   if (v < 0) {
@@ -594,17 +551,13 @@ bool fused_attention(int T, int H, int d, int K) {
 
 // encoder layers on the residual stream T.h; the first layer's LN1 output must already be in T.X.
 // Returns with the pooled rows in T.hc (pruned: *pooled_rows = true) or all rows in T.h.
-// ln_fold: the residual GEMMs (out_proj, fc2) also write the 16-bit residual copy into T.X and
-// per-row moments; ln_finalize turns them into (rstd, -rstd * mean) and the next GEMM (fc1 / the
-// next layer's qkv) runs on the copy with the LayerNorm folded into its weights and epilogue
-// (EPI_STORE_LN / EPI_GELU_LN): no LayerNorm kernel between GEMMs. The last layer's LN2 keeps
-// the LayerNorm kernel and the unfolded fc1 (its pooled rows are computed the same way pruned
-// or not).
+// (LayerNorm folded into the next GEMM -- producer moments in the residual epilogue, consumer
+// W diag(gamma) + epilogue correction -- was parity-green but 3 % slower end to end and was
+// removed: profiles/r02_v2_ln_fold_ab.txt.)
 int run_layers(clm_ctx* c, Tower& T, int B, int S, bool causal, const int32_t* ids, bool* pooled_rows,
                hipStream_t st, bool vl = false) {
   const bool bf = c->bf16();
   const bool prune = prune_last_layer();
-  const bool fold = c->ln_fold;
   *pooled_rows = false;
   // varlen (packed live text rows): the row-wise kernels read the live row count from
   // T.vl_counts; the profiled pass (no graph, may sync) counts the executed rows and attention pairs
@@ -617,31 +570,18 @@ int run_layers(clm_ctx* c, Tower& T, int B, int S, bool causal, const int32_t* i
     Mx = attn_pairs = 0;
     for (int v : lens) { Mx += v; attn_pairs += (double)v * v; }
   }
-  // residual GEMM that also produces the next LayerNorm's statistics (fold), then finalize them
-  auto resid_stats = [&](GemmArgs& g, int64_t M) -> int {
-    g.hb = T.X; g.ldhb = T.ldx; g.stats = T.stats;
-    { PROF(CLM_PROF_GEMM, 2.0 * M * g.N * g.K); KCHK(gemm(bf, EPI_RESID, g, st)); }
-    { PROF(CLM_PROF_LN, (double)M * (T.d / 32 * 8.0 + 8.0));
-      KCHK(ln_finalize(T.stats, T.d / 32, (int)M, c->desc.ln_eps, T.lnst, st)); }
-    return CLM_OK;
-  };
   // the pruned last layer's residual GEMMs have only B (pooled) rows: K is split into slices of
   // >= 4 K-steps (a fixed count per shape, so a row's bits do not depend on B), partials in the
-  // QKV workspace, which is idle by then (B * S rows * 3d 16-bit values)
-  static const bool pooled_small = !(getenv("CLM_POOLED_SPLITK") && !atoi(getenv("CLM_POOLED_SPLITK")));   // A/B switch
+  // QKV workspace, which is idle by then (B * S rows * 3d 16-bit values); 75 µs of idle chip per
+  // launch before (profiles/r02_v5_pooled_splitk_ab.txt)
   auto pooled_resid = [&](GemmArgs& g) -> int {
-    if (!pooled_small) {
-      PROF(CLM_PROF_GEMM, 2.0 * g.M * g.N * g.K);
-      KCHK(gemm(bf, EPI_RESID, g, st));
-      return CLM_OK;
-    }
     const int nk = g.K / 64;
     int slices = 1;
     for (int sl = nk / 4; sl >= 2; --sl)
       if (nk % sl == 0 && gemm_splitk_ws_bytes(1, g.N, sl) <= (size_t)S * 3 * T.d * 2) { slices = sl; break; }
     PROF(CLM_PROF_GEMM, 2.0 * g.M * g.N * g.K);
     if (slices > 1) KCHK(gemm_splitk_resid(bf, g, slices, (float*)T.QKV, st));
-    else KCHK(gemm_cfg(bf, EPI_RESID, 5, g, st));
+    else KCHK(gemm_cfg(bf, EPI_RESID, GEMM_CFG_SPLITK, g, st));
     return CLM_OK;
   };
   for (int l = 0; l < T.L; ++l) {
@@ -650,21 +590,17 @@ int run_layers(clm_ctx* c, Tower& T, int B, int S, bool causal, const int32_t* i
     int64_t M = (int64_t)B * S;
     GemmArgs g{};
     g.A = T.X; g.lda = T.ldx; g.M = (int)M; g.N = 3 * T.d; g.K = Lw.k_qkv; g.out = T.QKV; g.ldo = 3 * T.d;
-    if (fold && l > 0) {
-      g.W = Lw.w_qkv_f; g.ldw = Lw.k_qkv; g.bias = Lw.b_qkv_f; g.lnstat = T.lnst; g.cvec = Lw.c_qkv;
-    } else {
-      g.W = Lw.w_qkv; g.ldw = Lw.k_qkv; g.bias = Lw.b_qkv;
-    }
+    g.W = Lw.w_qkv; g.ldw = Lw.k_qkv; g.bias = Lw.b_qkv;
     if (vl) {   // packed live rows of variable-length captions
       PROF(CLM_PROF_GEMM, 2.0 * Mx * g.N * g.K + 4.0 * T.H * attn_pairs * 64);
       KCHK(gemm_attn_varlen(bf, causal, g.A, g.lda, g.W, g.ldw, g.bias, T.O, T.ldo, B, S, T.H, T.d, g.K, T.vl_lens,
                             T.vl_offs, T.vl_tiles, T.vl_counts, st));
-    } else if (!g.lnstat && fused_attention(S, T.H, T.d, g.K)) {
+    } else if (fused_attention(S, T.H, T.d, g.K)) {
       // one launch: the q/k/v GEMM's tiles attend their own sequences (GEMM + attention FLOPs)
       PROF(CLM_PROF_GEMM, 2.0 * M * g.N * g.K + 4.0 * B * T.H * (double)S * S * 64);
       KCHK(gemm_attn(bf, causal, g.A, g.lda, g.W, g.ldw, g.bias, T.O, T.ldo, B, S, T.H, T.d, g.K, st));
     } else {
-      { PROF(CLM_PROF_GEMM, 2.0 * M * g.N * g.K); KCHK(gemm(bf, g.lnstat ? EPI_STORE_LN : EPI_STORE, g, st)); }
+      { PROF(CLM_PROF_GEMM, 2.0 * M * g.N * g.K); KCHK(gemm(bf, EPI_STORE, g, st)); }
       { PROF(CLM_PROF_ATTN, 4.0 * B * T.H * (double)S * S * 64);
         KCHK(attention(bf, causal, T.QKV, 3 * T.d, T.O, T.ldo, B, S, T.H, T.d, st)); }
     }
@@ -685,20 +621,14 @@ int run_layers(clm_ctx* c, Tower& T, int B, int S, bool causal, const int32_t* i
     g = GemmArgs{};
     g.A = O; g.lda = T.ldo; g.W = Lw.w_out; g.ldw = Lw.k_out; g.M = (int)M; g.N = T.d; g.K = Lw.k_out;
     g.out = h; g.ldo = T.d; g.bias = Lw.b_out;
-    // the last layer's LN2 / fc1 always take the LayerNorm kernel (pooled rows or not), so the
-    // pruned and the every-row runs compute the pooled rows identically
-    const bool fold_mlp = fold && !last;
-    if (fold_mlp) {
-      int r = resid_stats(g, M);
+    if (pooled) {
+      int r = pooled_resid(g);
       if (r) return r;
     } else {
-      if (pooled) {
-        int r = pooled_resid(g);
-        if (r) return r;
-      } else {
-        g.m_dev = mdev;
-        PROF(CLM_PROF_GEMM, 2.0 * Mx * g.N * g.K); KCHK(gemm(bf, EPI_RESID, g, st));
-      }
+      g.m_dev = mdev;
+      PROF(CLM_PROF_GEMM, 2.0 * Mx * g.N * g.K); KCHK(gemm(bf, EPI_RESID, g, st));
+    }
+    {
       LnArgs ln = ln_into_x(c, T, M, Lw.ln2_g, Lw.ln2_b, Lw.a_fc1, Lw.r_fc1, h);
       if (!pooled) ln.m_dev = mdev;
       PROF(CLM_PROF_LN, (pooled ? (double)M : Mx) * T.d * 6.0);
@@ -706,37 +636,28 @@ int run_layers(clm_ctx* c, Tower& T, int B, int S, bool causal, const int32_t* i
     }
     g = GemmArgs{};
     g.A = T.X; g.lda = T.ldx; g.M = (int)M; g.N = T.mlp; g.K = Lw.k_fc1; g.out = T.Hm; g.ldo = T.ldm;
-    if (fold_mlp) {
-      g.W = Lw.w_fc1_f; g.ldw = Lw.k_fc1; g.bias = Lw.b_fc1_f; g.lnstat = T.lnst; g.cvec = Lw.c_fc1;
-    } else {
-      g.W = Lw.w_fc1; g.ldw = Lw.k_fc1; g.bias = Lw.b_fc1;
-    }
+    g.W = Lw.w_fc1; g.ldw = Lw.k_fc1; g.bias = Lw.b_fc1;
     if (!pooled) g.m_dev = mdev;
-    { PROF(CLM_PROF_GEMM, 2.0 * (pooled ? (double)M : Mx) * g.N * g.K);   // pooled rows: 64 x 128 tiles (config 5) fill the chip
-      KCHK(pooled && pooled_small ? gemm_cfg(bf, EPI_GELU, 5, g, st) : gemm(bf, g.lnstat ? EPI_GELU_LN : EPI_GELU, g, st)); }
+    { PROF(CLM_PROF_GEMM, 2.0 * (pooled ? (double)M : Mx) * g.N * g.K);   // pooled rows: 64 x 128 tiles fill the chip
+      KCHK(pooled ? gemm_cfg(bf, EPI_GELU, GEMM_CFG_SPLITK, g, st) : gemm(bf, EPI_GELU, g, st)); }
     if (Lw.r_fc2) { PROF(CLM_PROF_OTHER, 2.0 * M * T.mlp + 4.0 * Lw.r_fc2 * T.mlp);
       KCHK(lora_down(bf, T.Hm, T.ldm, (int)M, T.mlp, Lw.a_fc2, Lw.r_fc2, RPAD, st)); }
     g = GemmArgs{};
     g.A = T.Hm; g.lda = T.ldm; g.W = Lw.w_fc2; g.ldw = Lw.k_fc2; g.M = (int)M; g.N = T.d; g.K = Lw.k_fc2;
     g.out = h; g.ldo = T.d; g.bias = Lw.b_fc2;
-    if (!last && fold) {
-      int r = resid_stats(g, M);
+    if (pooled) {
+      int r = pooled_resid(g);
       if (r) return r;
     } else {
-      if (pooled) {
-        int r = pooled_resid(g);
-        if (r) return r;
-      } else {
-        g.m_dev = mdev;
-        PROF(CLM_PROF_GEMM, 2.0 * Mx * g.N * g.K); KCHK(gemm(bf, EPI_RESID, g, st));
-      }
-      if (!last) {
-        LayerW& Ln = T.layers[l + 1];
-        LnArgs ln = ln_into_x(c, T, M, Ln.ln1_g, Ln.ln1_b, Ln.a_qkv, Ln.r_qkv);
-        ln.m_dev = mdev;
-        PROF(CLM_PROF_LN, Mx * T.d * 6.0);
-        KCHK(layernorm(bf, ln, st));
-      }
+      g.m_dev = mdev;
+      PROF(CLM_PROF_GEMM, 2.0 * Mx * g.N * g.K); KCHK(gemm(bf, EPI_RESID, g, st));
+    }
+    if (!last) {
+      LayerW& Ln = T.layers[l + 1];
+      LnArgs ln = ln_into_x(c, T, M, Ln.ln1_g, Ln.ln1_b, Ln.a_qkv, Ln.r_qkv);
+      ln.m_dev = mdev;
+      PROF(CLM_PROF_LN, Mx * T.d * 6.0);
+      KCHK(layernorm(bf, ln, st));
     }
   }
   return CLM_OK;
@@ -751,8 +672,6 @@ Tower ws_view(const Tower& T0, int b0, int rows, int patches, int proj_dim) {
   T.pooled += (int64_t)b0 * proj_dim;
   T.hc += (int64_t)b0 * T.d;
   T.Oc += (int64_t)b0 * T.ldo;
-  if (T.stats) T.stats += r0 * (T.d / 32);
-  if (T.lnst) T.lnst += r0;
   if (T.vl_lens) {
     T.vl_lens += b0; T.vl_tiles += b0; T.vl_offs += 2 * b0; T.vl_counts += 2 * b0; T.vl_rowmap += r0;
   }
@@ -792,7 +711,7 @@ int encode_text_chunk(clm_ctx* c, Tower& T, const int32_t* ids_dev, int B, int L
   a.hf = T.h; a.ldh = T.d; a.g1 = T.layers[0].ln1_g; a.b1 = T.layers[0].ln1_b;
   a.y = T.X; a.ldy = T.ldx; a.loraA = T.layers[0].a_qkv; a.r_ext = T.layers[0].r_qkv;
   a.r_pad = a.loraA ? RPAD : 0; a.M = B * L; a.d = T.d; a.eps = d.ln_eps;
-  bool vl = text_varlen_enabled() && T.vl_lens && !c->ln_fold && B <= 4096 &&   // text_plan: <= 4096 captions per chunk
+  bool vl = text_varlen_enabled() && T.vl_lens && B <= 4096 &&   // text_plan: <= 4096 captions per chunk
             fused_attention(L, T.H, T.d, T.layers.empty() ? 0 : T.layers[0].k_qkv);
   for (const LayerW& Lw : T.layers) vl = vl && !Lw.r_qkv && !Lw.r_out && !Lw.r_fc1 && !Lw.r_fc2;
   if (vl) {
@@ -977,13 +896,6 @@ int clm_finalize(clm_ctx* ctx) {
   (void)hipDeviceSynchronize();
   ctx->free_all();
   ctx->finalized = false;
-  {
-    // opt-in ($CLM_LN_FOLD=1): measured 3 % slower end to end on MI355X (45.2k vs 46.75k pairs/s,
-    // profiles/r02_v2_ln_fold_ab.txt) -- the extra epilogue work of the residual GEMMs (16-bit
-    // copy + moments) and of the folded qkv / fc1 GEMMs costs more than the LayerNorm kernels
-    const char* e = getenv("CLM_LN_FOLD");
-    ctx->ln_fold = ctx->desc.lora_mode == CLM_LORA_MERGED && e && atoi(e) == 1;
-  }
   int r = build_tower(ctx, ctx->vis, true);
   if (!r) r = build_tower(ctx, ctx->txt, false);
   if (!r) r = ctx->dalloc(&ctx->ids_dev, (size_t)ctx->desc.max_batch * ctx->desc.max_pos);

@@ -7,64 +7,20 @@
 
 #include "kernels.hpp"
 
-// cache policy of the epilogue's output stores (experiment build -DCLM_STORE_AUX=16: sc1, which
-// writes through and drops the line from the XCD's L2 instead of keeping it)
-#ifndef CLM_STORE_AUX
-#define CLM_STORE_AUX 0
-#endif
-
 namespace clm {
 namespace gemm_detail {
-// percentage of the resident workgroup slots a persistent GEMM grid takes ($CLM_GEMM_GRID_PCT,
-// default 100): below 100 two GEMMs on different streams (image / text towers) can share the chip
-inline int grid_pct() {
-  static int pct = -1;
-  if (pct < 0) {
-    const char* e = getenv("CLM_GEMM_GRID_PCT");
-    pct = e ? std::max(1, std::min(100, atoi(e))) : 100;
-  }
-  return pct;
-}
-// banded persistent tile walk (tile_walk below), $CLM_GEMM_BAND=1; off by default: it left the
-// GEMMs' L2 hit rate (71-86 %) and the pair step unchanged (profiles/r02_v6_gemm_band_ab.txt)
-inline int gemm_band() {
-  static int v = -1;
-  if (v < 0) {
-    const char* e = getenv("CLM_GEMM_BAND");
-    v = (e && atoi(e)) ? 1 : 0;
-  }
-  return v;
-}
-// grouped-raster row panels per group ($CLM_GEMM_GM). 4: an XCD's 32 concurrent tiles cover 4
-// row panels x 8 column tiles, fewer unique operand bytes per round than 8 x 4 (Infinity-Cache
-// traffic is the main loops' bound): pair step +0.9 % vs 8, 16 -3.7 %, 2 +0.2 %
+// grouped raster: row panels per group. 4: an XCD's 32 concurrent tiles cover 4 row panels x 8
+// column tiles, fewer unique operand bytes per round than 8 x 4 (Infinity-Cache traffic is the main
+// loops' bound): pair step +0.9 % vs 8, 16 -3.7 %, 2 +0.2 %
 // (profiles/r02_v6_gemm_raster_ab.txt)
-inline int gemm_gm() {
-  static int v = -1;
-  if (v < 0) {
-    const char* e = getenv("CLM_GEMM_GM");
-    v = e ? std::max(1, std::min(64, atoi(e))) : 4;
-  }
-  return v;
-}
+constexpr int GM = 4;
 constexpr int BK = 64;
 
-// Persistent tile walk of workgroup blockIdx.x over `ntiles` tiles with G workgroups.
-// Banded (GemmArgs::band, $CLM_GEMM_BAND=1): the tile order is cut into 8 contiguous bands, one per XCD
-// group (blocks b = x mod 8 share an XCD under the round-robin dispatch; which XCD is not assumed,
-// only that they share one -- a wrong guess costs speed, never correctness), and the group's
-// workgroups walk their band round by round, so each XCD's L2 keeps serving the same row-panel
-// group instead of every XCD sweeping the whole tile space. Otherwise workgroup xb (the bijective
-// XCD remap) takes tiles xb, xb + G, ...
+// Persistent tile walk of workgroup blockIdx.x over `ntiles` tiles with G workgroups: workgroup xb
+// (the bijective XCD remap) takes tiles xb, xb + G, ... (a banded walk, one band of the tile order
+// per XCD group, left the L2 hit rate and the pair step unchanged: profiles/r02_v6_gemm_band_ab.txt)
 struct TileWalk { int first, stride, count; };
-__device__ __forceinline__ TileWalk tile_walk(int ntiles, int G, bool band) {
-  if (band && G >= 8) {
-    const int x = blockIdx.x % 8, j = blockIdx.x / 8;
-    const int nx = (G - x + 7) / 8;   // workgroups of this XCD group
-    const int lo = (int)((int64_t)ntiles * x / 8), hi = (int)((int64_t)ntiles * (x + 1) / 8);
-    const int n = hi - lo;
-    return TileWalk{lo + j, nx, j < n ? (n - j + nx - 1) / nx : 0};
-  }
+__device__ __forceinline__ TileWalk tile_walk(int ntiles, int G) {
   const int xb = xcd_remap(blockIdx.x, G);
   return TileWalk{xb, G, xb < ntiles ? (ntiles - 1 - xb) / G + 1 : 0};
 }
@@ -121,7 +77,6 @@ __device__ __forceinline__ void epilogue_scalar(const GemmArgs& g, const f32x4 (
         const int nj = wcol + nb * 16 + j;
         if (nj >= g.N) break;
         float x = acc[mb][nb][j];
-        if constexpr (epi_ln(EPI)) x = x * g.lnstat[m].x + g.lnstat[m].y * g.cvec[nj];   // LayerNorm folding
         if constexpr (epi_stores16(EPI) || EPI == EPI_RESID)
           if (g.bias) x += g.bias[nj];
         if constexpr (epi_stores16(EPI) && !epi_gelu(EPI)) ((u16*)g.out)[(int64_t)m * g.ldo + nj] = from_f32<BF>(x);
@@ -167,10 +122,6 @@ __device__ __forceinline__ void epilogue(const GemmArgs& g, const f32x4 (&acc)[B
   // path with TN > 4 loads them per row-block instead (VGPR budget, see below)
   constexpr bool HOIST = !(EPI == EPI_RESID || EPI == EPI_PATCH) || C::TN <= 4;
   float4 cv[C::TN];
-  // LayerNorm folding: the column sums of W' too, loaded with the bias before any store (a load
-  // issued after a store waits for that store's round trip); only TN <= 4 tiles take it
-  static_assert(!epi_ln(EPI) || C::TN <= 4, "LayerNorm-folded epilogues: TN <= 4 tiles");
-  float4 cv2[epi_ln(EPI) ? C::TN : 1];
 #pragma unroll
   for (int nb = 0; nb < C::TN; ++nb) {
     if constexpr (!HOIST) break;
@@ -179,27 +130,12 @@ __device__ __forceinline__ void epilogue(const GemmArgs& g, const f32x4 (&acc)[B
       cv[nb] = (g.cscale && n < g.N) ? *(const float4*)(g.cscale + n) : make_float4(1.f, 1.f, 1.f, 1.f);
     else
       cv[nb] = (g.bias && n < g.N) ? *(const float4*)(g.bias + n) : make_float4(0.f, 0.f, 0.f, 0.f);
-    if constexpr (epi_ln(EPI)) cv2[nb] = n < g.N ? *(const float4*)(g.cvec + n) : make_float4(0.f, 0.f, 0.f, 0.f);
   }
 
   if constexpr (epi_stores16(EPI)) {
-    float2 ls[epi_ln(EPI) ? C::TM : 1];   // LayerNorm folding: per row (rstd, -rstd * mean)
-#pragma unroll
-    for (int mb = 0; mb < C::TM; ++mb) {
-      if constexpr (!epi_ln(EPI)) break;
-      const int m = wrow + mb * 16;
-      ls[mb] = m < g.M ? g.lnstat[m] : make_float2(1.f, 0.f);
-    }
     auto finish = [&](int mb, int nb) {
       float v[4] = {acc[mb][nb][0] + cv[nb].x, acc[mb][nb][1] + cv[nb].y, acc[mb][nb][2] + cv[nb].z,
                     acc[mb][nb][3] + cv[nb].w};
-      if constexpr (epi_ln(EPI)) {
-        const float a = ls[mb].x, b = ls[mb].y;
-        v[0] = fmaf(acc[mb][nb][0], a, fmaf(b, cv2[nb].x, cv[nb].x));
-        v[1] = fmaf(acc[mb][nb][1], a, fmaf(b, cv2[nb].y, cv[nb].y));
-        v[2] = fmaf(acc[mb][nb][2], a, fmaf(b, cv2[nb].z, cv[nb].z));
-        v[3] = fmaf(acc[mb][nb][3], a, fmaf(b, cv2[nb].w, cv[nb].w));
-      }
       if constexpr (epi_gelu(EPI)) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) v[j] = quick_gelu(v[j]);
@@ -224,7 +160,7 @@ __device__ __forceinline__ void epilogue(const GemmArgs& g, const f32x4 (&acc)[B
           const auto ry = __builtin_amdgcn_permlane16_swap(p0.y, p1.y, false, false);
           const int col = wcol8 + nb * 16;
           const uint32_t off = (m < g.M && col < g.N) ? (uint32_t)(((m - m0) * g.ldo + col) * 2) : BUF_OOB;
-          __builtin_amdgcn_raw_buffer_store_b128(u32x4{rx[0], ry[0], rx[1], ry[1]}, ob, off, 0, CLM_STORE_AUX);
+          __builtin_amdgcn_raw_buffer_store_b128(u32x4{rx[0], ry[0], rx[1], ry[1]}, ob, off, 0, 0);
         }
       }
     } else {
@@ -235,7 +171,7 @@ __device__ __forceinline__ void epilogue(const GemmArgs& g, const f32x4 (&acc)[B
         for (int nb = 0; nb < C::TN; ++nb) {
           const int n = wcol + nb * 16;
           const uint32_t off = (m < g.M && n < g.N) ? (uint32_t)(((m - m0) * g.ldo + n) * 2) : BUF_OOB;
-          __builtin_amdgcn_raw_buffer_store_b64(finish(mb, nb), ob, off, 0, CLM_STORE_AUX);
+          __builtin_amdgcn_raw_buffer_store_b64(finish(mb, nb), ob, off, 0, 0);
         }
       }
     }
@@ -277,21 +213,11 @@ __device__ __forceinline__ void epilogue(const GemmArgs& g, const f32x4 (&acc)[B
     // pipelining holds 2 * TN float4 of loaded rows; where that would cost a wave per SIMD
     // (TN > 4, or PATCH's extra address VALU) one block at a time is loaded, then stored
     constexpr bool PIPE = EPI == EPI_RESID && C::TN <= 4;
-    // LayerNorm-folding producer (GemmArgs::stats): the 16-bit copy of each new residual row
-    // and, per row and 32-column chunk (2 consecutive 16-column blocks; every wave's column
-    // span is a multiple of 32), the chunk's mean and M2 (two passes over values kept in
-    // registers, then the 4 lane groups) in slot n / 32 of N / 32
-    const bool st = EPI == EPI_RESID && g.stats != nullptr;
-    const auto hbb = buf_rsrc(st ? (const void*)(g.hb + (int64_t)m0 * g.ldhb) : g.out, nrec);
-    const auto sb = buf_rsrc(st ? (const void*)(g.stats + (int64_t)m0 * (g.N / 32)) : g.out, nrec);
-    static_assert(EPI != EPI_RESID || C::TN % 2 == 0, "moment chunks need an even number of column blocks");
     u32x4 hc[C::TN], hn[C::TN];
     load_blk(0, hc);
 #pragma unroll
     for (int mb = 0; mb < C::TM; ++mb) {
       if (PIPE && mb + 1 < C::TM) load_blk(mb + 1, hn);
-      float4 rv[C::TN];
-      u32x2 hpend{0u, 0u};
 #pragma unroll
       for (int nb = 0; nb < C::TN; ++nb) {
         uint32_t oo, ao;
@@ -302,46 +228,7 @@ __device__ __forceinline__ void epilogue(const GemmArgs& g, const f32x4 (&acc)[B
         const float r2 = __uint_as_float(hc[nb][2]) + (acc[mb][nb][2] + c.z);
         const float r3 = __uint_as_float(hc[nb][3]) + (acc[mb][nb][3] + c.w);
         __builtin_amdgcn_raw_buffer_store_b128(
-            u32x4{__float_as_uint(r0), __float_as_uint(r1), __float_as_uint(r2), __float_as_uint(r3)}, ob, oo, 0,
-            CLM_STORE_AUX);
-        if (st) {
-          // 16-B stores of the 16-bit copy: as the STORE epilogue's wide path, v_permlane16_swap
-          // gives lane group q the 8 consecutive columns (nb-1 + (q & 1)) * 16 + (q >> 1) * 8 ..
-          const u32x2 cur{pack2<BF>(r0, r1), pack2<BF>(r2, r3)};
-          if (nb % 2 == 0) {
-            hpend = cur;
-          } else {
-            const auto rx = __builtin_amdgcn_permlane16_swap(hpend.x, cur.x, false, false);
-            const auto ry = __builtin_amdgcn_permlane16_swap(hpend.y, cur.y, false, false);
-            const int m = wrow + mb * 16, q = lane >> 4;
-            const int col = n0 + wn * (BN / WN) + (q & 1) * 16 + (q >> 1) * 8 + (nb - 1) * 16;
-            const uint32_t ho = (m < g.M && col < g.N) ? (uint32_t)(((int64_t)(m - m0) * g.ldhb + col) * 2) : BUF_OOB;
-            __builtin_amdgcn_raw_buffer_store_b128(u32x4{rx[0], ry[0], rx[1], ry[1]}, hbb, ho, 0, 0);
-          }
-          rv[nb] = make_float4(r0, r1, r2, r3);
-        }
-      }
-      if (st) {
-        const int m = wrow + mb * 16;
-#pragma unroll
-        for (int ch = 0; ch < C::TN / 2; ++ch) {
-          const float4 a = rv[2 * ch], b = rv[2 * ch + 1];
-          float s1 = ((a.x + a.y) + (a.z + a.w)) + ((b.x + b.y) + (b.z + b.w));
-          s1 += __shfl_xor(s1, 16, 64);
-          s1 += __shfl_xor(s1, 32, 64);
-          const float mean = s1 * (1.0f / 32.0f);
-          const float e0 = a.x - mean, e1 = a.y - mean, e2 = a.z - mean, e3 = a.w - mean;
-          const float f0 = b.x - mean, f1 = b.y - mean, f2 = b.z - mean, f3 = b.w - mean;
-          float s2 = ((e0 * e0 + e1 * e1) + (e2 * e2 + e3 * e3)) + ((f0 * f0 + f1 * f1) + (f2 * f2 + f3 * f3));
-          s2 += __shfl_xor(s2, 16, 64);
-          s2 += __shfl_xor(s2, 32, 64);
-          const int n = wcol - (lane >> 4) * 4 + ch * 32;   // chunk's first column
-          // predicated by the buffer range check, not a branch (a branch per store makes the
-          // waitcnt pass drain vmcnt in front of every store)
-          const uint32_t so = ((lane >> 4) == 0 && m < g.M && n < g.N)
-                                  ? (uint32_t)(((int64_t)(m - m0) * (g.N / 32) + n / 32) * 8) : BUF_OOB;
-          __builtin_amdgcn_raw_buffer_store_b64(u32x2{__float_as_uint(mean), __float_as_uint(s2)}, sb, so, 0, 0);
-        }
+            u32x4{__float_as_uint(r0), __float_as_uint(r1), __float_as_uint(r2), __float_as_uint(r3)}, ob, oo, 0, 0);
       }
       if (mb + 1 < C::TM) {
         if constexpr (PIPE) {
@@ -414,8 +301,6 @@ constexpr int epi_min_stores() {
 
 }  // namespace gemm_detail
 
-// G2 kernels (k_gemm2.hip): configs 11-22
+// G2 kernels (k_gemm2.hip): configs 8-11
 hipError_t gemm2_launch(bool bf16, int epi, int id, const GemmArgs& g, hipStream_t s);
-// G3 kernel (k_gemm3.hip): config 23, 256 x 256 eight-phase ping-pong
-hipError_t gemm3_launch(bool bf16, int epi, const GemmArgs& g, hipStream_t s);
 }  // namespace clm

@@ -29,8 +29,7 @@ namespace clm {
 
 namespace {
 using namespace gemm_detail;
-// Persistent: workgroup b walks its tiles (tile_walk: one contiguous band per XCD group, G =
-// gridDim.x <= tiles workgroups), and its LDS-DMA ring runs ACROSS tile boundaries: the first
+// Persistent: workgroup b walks its tiles (tile_walk, G = gridDim.x <= tiles workgroups), and its LDS-DMA ring runs ACROSS tile boundaries: the first
 // K-tiles of tile i+1 are issued before tile i's epilogue, so they land while the epilogue
 // runs, and the epilogue's stores drain under tile i+1's main loop (counted vmcnt that
 // leaves them in flight). A one-tile-per-workgroup grid is the plain non-persistent GEMM.
@@ -45,7 +44,7 @@ __global__ __launch_bounds__(WM * WN * 64, (Cfg<BM, BN, WM, WN, STAGES>::WAVES_P
   const int ntn = (g.N + BN - 1) / BN, ntm = (g.M + BM - 1) / BM;
   const int ks = g.ksplit > 1 ? g.ksplit : 1;   // split-K: work unit = (tile, K slice)
   const int ntiles = ntn * ntm * ks, G = gridDim.x;
-  const TileWalk tw = tile_walk(ntiles, G, g.band != 0);
+  const TileWalk tw = tile_walk(ntiles, G);
   if (tw.count <= 0) return;   // varlen: fewer live tiles than the grid
   const int n_my = tw.count;
   const int nk = g.K / BK / ks;
@@ -63,7 +62,7 @@ __global__ __launch_bounds__(WM * WN * 64, (Cfg<BM, BN, WM, WN, STAGES>::WAVES_P
       tm = t % ntm;
       tn = t / ntm;
     } else {                    // grouped raster: GM row-panels x all N-tiles per group, M inner,
-      const int GM = g.gm > 0 ? g.gm : 4;     // so an XCD's concurrent tiles share A panels and W tiles in L2
+                                // so an XCD's concurrent tiles share A panels and W tiles in L2
       const int group = t / (GM * ntn);
       const int first_m = group * GM;
       const int gsz = min(GM, ntm - first_m);
@@ -211,44 +210,34 @@ hipError_t launch_cfg(const GemmArgs& g, hipStream_t s) {
     sl = per_cu * cus;
   }
   const int tiles = ((g.N + BN - 1) / BN) * ((g.M + BM - 1) / BM) * (g.ksplit > 1 ? g.ksplit : 1);
-  const int nwg = (g.debug & 4) ? tiles : std::min(tiles, std::max(1, sl * grid_pct() / 100));   // debug bit 2: one tile per workgroup
-  GemmArgs ga = g;
-  ga.band = gemm_band();
-  ga.gm = gemm_gm();
-  kern<<<dim3(nwg), dim3(C::NT), C::LDS, s>>>(ga);
+  const int nwg = (g.debug & 4) ? tiles : std::min(tiles, sl);   // debug bit 2: one tile per workgroup
+  kern<<<dim3(nwg), dim3(C::NT), C::LDS, s>>>(g);
   return hipGetLastError();
 }
 
-// tile configurations (index = GemmArgs-independent id, also the `config` of clm_gemm)
+// tile configurations (index = GemmArgs-independent id, also the `config` of clm_gemm); every one
+// is picked by pick_config for some shape. Configs that never won inside the encode pipeline
+// (other gemm_kernel / G2 tiles, G2's deferred-store and 3-buffer twins, the 256 x 256
+// eight-phase G3) were removed; their A/B records stay under profiles/ (r01_v8_*, r01_v10_*,
+// r02_v4_*, r02_v9_tile_family_ab.txt).
 template <bool BF, int EPI>
 hipError_t launch_id(int id, const GemmArgs& g, hipStream_t s) {
-  if constexpr (epi_ln(EPI)) {   // LayerNorm-folded epilogues: the TN <= 4 tiles of G2 / G3 only
-    if (id == 23) return gemm3_launch(BF, EPI, g, s);
-    if (id >= 16 && id <= 18) return gemm2_launch(BF, EPI, id, g, s);
-    return hipErrorInvalidValue;
-  } else {
   switch (id) {
     case 0: return launch_cfg<BF, EPI, 128, 128, 2, 2, 2>(g, s);
-    case 1: return launch_cfg<BF, EPI, 128, 128, 2, 2, 3>(g, s);
-    case 2: return launch_cfg<BF, EPI, 256, 128, 4, 2, 3>(g, s);
-    case 3: return launch_cfg<BF, EPI, 128, 256, 2, 4, 3>(g, s);
-    case 4: return launch_cfg<BF, EPI, 256, 256, 4, 2, 2>(g, s);
-    case 5: return launch_cfg<BF, EPI, 64, 128, 1, 2, 3>(g, s);
-    case 6: return launch_cfg<BF, EPI, 128, 192, 2, 2, 2>(g, s);
-    case 7: return launch_cfg<BF, EPI, 192, 128, 2, 2, 2>(g, s);
-    case 8: return launch_cfg<BF, EPI, 256, 128, 4, 2, 2>(g, s);
-    case 9: return launch_cfg<BF, EPI, 192, 192, 2, 2, 2>(g, s);
-    case 10: return launch_cfg<BF, EPI, 128, 256, 2, 4, 2>(g, s);
-    case 11: case 12: case 13: case 14: case 15: case 16: case 17: case 18: case 19: case 20: case 21: case 22:
-      return gemm2_launch(BF, EPI, id, g, s);
-    case 23: return gemm3_launch(BF, EPI, g, s);
-    case 24: return launch_cfg<BF, EPI, 160, 128, 2, 2, 2>(g, s);
+    case 1: return launch_cfg<BF, EPI, 256, 256, 4, 2, 2>(g, s);
+    case 2: return launch_cfg<BF, EPI, 64, 128, 1, 2, 3>(g, s);
+    case 3: return launch_cfg<BF, EPI, 128, 192, 2, 2, 2>(g, s);
+    case 4: return launch_cfg<BF, EPI, 192, 128, 2, 2, 2>(g, s);
+    case 5: return launch_cfg<BF, EPI, 256, 128, 4, 2, 2>(g, s);
+    case 6: return launch_cfg<BF, EPI, 128, 256, 2, 4, 2>(g, s);
+    case 7: return launch_cfg<BF, EPI, 160, 128, 2, 2, 2>(g, s);
+    case 8: case 9: case 10: case 11: return gemm2_launch(BF, EPI, id, g, s);
     default: return hipErrorInvalidValue;
-  }
   }
 }
 
-constexpr int NCFG = 25;
+constexpr int NCFG = 12;
+static_assert(GEMM_CFG_SPLITK == 2, "config 2 is the 64 x 128 tile");
 
 // Tile choice: a cost model per kernel family, time(cfg) ~ rounds(cfg) x round_cost(cfg),
 // rounds = ceil(tiles / resident workgroups), round_cost = BM*BN*(workgroups per CU) /
@@ -264,26 +253,27 @@ constexpr int NCFG = 25;
 //    read-modify-write outputs (out_proj / fc2 RESID, patch PATCH) take the 2-workgroups-per-CU
 //    tiles (192x128 / 128x192), whose co-resident workgroups overlap one tile's residual round
 //    trip with the other's MFMAs.
-// $CLM_GEMM_CFG overrides.
+// $CLM_GEMM_CFG forces a config (tools and tests).
 struct CfgModel { int id, bm, bn, wg_per_cu; double eff; };
 constexpr CfgModel MODELS_G2[] = {
-  {15, 256, 192, 1, 2.569}, {16, 256, 128, 1, 2.349}, {17, 192, 256, 1, 2.521}, {18, 128, 256, 1, 2.340}};
-// 160x128 (config 24): the N = 512 / 768 RESID / PATCH shapes fill one round of 2-WG/CU slots
+  {8, 256, 192, 1, 2.569}, {9, 256, 128, 1, 2.349}, {10, 192, 256, 1, 2.521}, {11, 128, 256, 1, 2.340}};
+// 160x128 (config 7): the N = 512 / 768 RESID / PATCH shapes fill one round of 2-WG/CU slots
 // (480 / 496 tiles of 512, against 402 / 412 with 192x128): v_out 28.7 vs 32.0 µs, v_fc2 67.7
-// vs 74.9, t_out 24.0 vs 25.8, t_fc2 49.5 vs 53.7 (profiles/r02_v4_gemm_160x128.txt)
+// vs 74.9, t_out 24.0 vs 25.8, t_fc2 49.5 vs 53.7 (profiles/r02_v4_gemm_160x128.txt) -- when the
+// GEMM has the chip to itself; while the two towers run concurrently (gemm_set_concurrent) it is
+// skipped: the 192x128 / 128x192 single round leaves ~20 % of the slots to the other stream
+// (profiles/r02_v9_tile_family_ab.txt)
 constexpr CfgModel MODELS[] = {
-  {0, 128, 128, 2, 0.975}, {4, 256, 256, 1, 1.18}, {6, 128, 192, 2, 0.955}, {7, 192, 128, 2, 0.955},
-  {8, 256, 128, 1, 1.025}, {10, 128, 256, 1, 1.056}, {24, 160, 128, 2, 0.93}};
+  {0, 128, 128, 2, 0.975}, {1, 256, 256, 1, 1.18}, {3, 128, 192, 2, 0.955}, {4, 192, 128, 2, 0.955},
+  {5, 256, 128, 1, 1.025}, {6, 128, 256, 1, 1.056}, {7, 160, 128, 2, 0.93}};
 thread_local bool g_concurrent = false;
 template <int NM>
 int pick_from(const CfgModel (&models)[NM], int M, int N) {
-  static const long long env_skip = getenv("CLM_GEMM_SKIP_MASK") ? atoll(getenv("CLM_GEMM_SKIP_MASK")) : 0;   // A/B: bit per config id
-  static const bool conc_tiles = !(getenv("CLM_CONC_TILES") && !atoi(getenv("CLM_CONC_TILES")));   // A/B switch
-  const long long skip = env_skip | (g_concurrent && conc_tiles ? (1LL << 24) : 0);
+  const int skip = g_concurrent ? 7 : -1;
   int best = models[0].id;
   double best_cost = 1e300;
   for (const CfgModel& c : models) {
-    if ((skip >> c.id) & 1) continue;
+    if (c.id == skip) continue;
     const int64_t tiles = (int64_t)((M + c.bm - 1) / c.bm) * ((N + c.bn - 1) / c.bn);
     const int64_t slots = 256LL * c.wg_per_cu;
     const int64_t rounds = (tiles + slots - 1) / slots;
@@ -298,40 +288,13 @@ int pick_config(int epi, int M, int N) {
     const char* e = getenv("CLM_GEMM_CFG");
     forced = e ? atoi(e) : -1;
   }
-  if (epi_ln(epi)) {   // LayerNorm-folded epilogues (TN <= 4 tiles): qkv -> G3, fc1 -> G2 16 / 17 / 18
-    if (forced == 23 || (forced >= 16 && forced <= 18)) return forced;
-    if (epi == EPI_STORE_LN) return 23;
-    constexpr CfgModel MODELS_LN[] = {{16, 256, 128, 1, 2.349}, {17, 192, 256, 1, 2.521}, {18, 128, 256, 1, 2.340}};
-    return pick_from(MODELS_LN, M, N);
-  }
   if (forced >= 0 && forced < NCFG) return forced;
-  static int g2_epis = -1;   // epilogues served by G2 (bit per Epi); $CLM_G2_EPIS overrides
-  if (g2_epis < 0) {
-    const char* e = getenv("CLM_G2_EPIS");
-    g2_epis = e ? atoi(e) : (1 << EPI_GELU);
-  }
-  // G2 16 / 18 -> their deferred-store twins 19 / 20 ($CLM_G2_DEFER=1). Off: spreading a
-  // tile's stores over the next tile's K-steps made fc1 7 % slower in the pipeline (the stores
-  // share the CU's memory path with the main loop's LDS-DMA), against the burst epilogue.
-  static int defer = -1;
-  if (defer < 0) {
-    const char* e = getenv("CLM_G2_DEFER");
-    defer = e ? atoi(e) : 0;
-  }
-  static int stages = -1;   // G2 16 / 18 -> their 3-buffer-ring twins 21 / 22; $CLM_G2_STAGES
-  if (stages < 0) {
-    const char* e = getenv("CLM_G2_STAGES");
-    stages = e ? atoi(e) : 2;
-  }
-  if (!((g2_epis >> epi) & 1)) return pick_from(MODELS, M, N);
+  if (epi != EPI_GELU) return pick_from(MODELS, M, N);
   // Large M (>= 4 full rounds of 256 x 256 tiles, e.g. ViT-L/14@336 batch 128: fc1 73,856 x 4,096):
   // quantisation no longer favours G2's narrower tiles: gemm_kernel 256 x 256 takes 636 us there
   // against 874 for G2 256 x 128 (tools/quant_probe.py, profiles/r02_v6_l14_gemm_probe.txt)
-  if (epi == EPI_GELU && (int64_t)((M + 255) / 256) * ((N + 255) / 256) >= 4 * 256) return 4;
-  const int id = pick_from(MODELS_G2, M, N);
-  if (stages == 3) return id == 16 ? 21 : id == 18 ? 22 : id;
-  if (defer && (epi == EPI_STORE || epi == EPI_GELU)) return id == 16 ? 19 : id == 18 ? 20 : id;
-  return id;
+  if ((int64_t)((M + 255) / 256) * ((N + 255) / 256) >= 4 * 256) return 1;
+  return pick_from(MODELS_G2, M, N);
 }
 
 template <bool BF>
@@ -343,8 +306,6 @@ hipError_t dispatch(int epi, int id, const GemmArgs& g, hipStream_t s) {
     case EPI_PATCH: return launch_id<BF, EPI_PATCH>(id, g, s);
     case EPI_SCORE: return launch_id<BF, EPI_SCORE>(id, g, s);
     case EPI_FILTER: return launch_id<BF, EPI_FILTER>(id, g, s);
-    case EPI_STORE_LN: return launch_id<BF, EPI_STORE_LN>(id, g, s);
-    case EPI_GELU_LN: return launch_id<BF, EPI_GELU_LN>(id, g, s);
     default: return hipErrorInvalidValue;
   }
 }
@@ -361,26 +322,6 @@ hipError_t gemm_cfg(bool bf16, int epi, int config, const GemmArgs& g, hipStream
 
 hipError_t gemm(bool bf16, int epi, const GemmArgs& g, hipStream_t s) {
   if (g.ksplit > 1) return hipErrorInvalidValue;   // split-K: gemm_splitk_resid only
-  // $CLM_GEMM_MSPLIT=1 (experiment, off: 4 % slower in the two-tower pipeline, whose other tower
-  // already fills a partial round; profiles/r02_v6_gemm_msplit_ab.txt): a quick-GELU GEMM whose 256 x 256 tiles fill at least one
-  // full round of the 256 CUs runs as two launches on the same stream -- the row panels of the
-  // full rounds with gemm_kernel 256 x 256, the remaining rows with the heuristic's tile -- so
-  // the last, partial round is of smaller tiles. Rows are independent and every tile config
-  // gives the same bits, so the results are unchanged.
-  static const bool msplit = getenv("CLM_GEMM_MSPLIT") && atoi(getenv("CLM_GEMM_MSPLIT"));
-  if (msplit && epi == EPI_GELU && !g.m_dev && g.M > 0 && g.N > 0) {
-    const int64_t ntn = (g.N + 255) / 256, ntm = (g.M + 255) / 256, tiles = ntn * ntm;
-    const int64_t M1 = (tiles / 256) * 256 / ntn * 256;   // whole 256-row panels of the full rounds
-    if (M1 > 0 && M1 < g.M && tiles % 256) {
-      GemmArgs a = g, b = g;
-      a.M = (int)M1;
-      b.M = g.M - (int)M1;
-      b.A = g.A + M1 * g.lda;
-      b.out = (u16*)g.out + M1 * g.ldo;
-      hipError_t e = gemm_cfg(bf16, epi, 4, a, s);
-      return e != hipSuccess ? e : gemm_cfg(bf16, epi, -1, b, s);
-    }
-  }
   return gemm_cfg(bf16, epi, -1, g, s);
 }
 
@@ -413,8 +354,8 @@ hipError_t gemm_splitk_resid(bool bf16, const GemmArgs& g, int slices, float* ws
   GemmArgs p = g;   // slice partials: EPI_SCORE with no scales stores acc * 1 * 1 = acc exactly
   p.out = ws; p.ldo = g.N; p.bias = nullptr; p.rscale = nullptr; p.cscale = nullptr;
   p.ksplit = slices; p.split_stride = (int64_t)g.M * g.N;
-  // 64 x 128 tiles (config 5): the few rows still spread over many workgroups
-  hipError_t e = gemm_cfg(bf16, EPI_SCORE, 5, p, s);
+  // 64 x 128 tiles: the few rows still spread over many workgroups
+  hipError_t e = gemm_cfg(bf16, EPI_SCORE, GEMM_CFG_SPLITK, p, s);
   if (e != hipSuccess) return e;
   const int64_t n = (int64_t)g.M * (g.N / 4);
   splitk_resid_kernel<<<(unsigned)((n + 255) / 256), 256, 0, s>>>(ws, slices, g.M, g.N, g.bias, (float*)g.out, g.ldo);

@@ -1,4 +1,4 @@
-// G2 MFMA GEMM for gfx950 (configs 11-13 of clm_gemm): one wave per SIMD with large per-wave
+// G2 MFMA GEMM for gfx950 (configs 8-11 of clm_gemm): one wave per SIMD with large per-wave
 // tiles, for the encoder's dense qkv / out / fc1 / fc2 GEMMs (TF/models/clip/modeling_clip.py:
 // 294-297, 332, 343-344). Same operand layout, epilogues and persistent tile order as
 // k_gemm.hip's gemm_kernel; the main loop differs (see below).
@@ -19,14 +19,14 @@ using namespace gemm_detail;
 // The LDS latency of every fragment read is covered by 64 MFMAs of the other half, the only
 // MFMA-idle window per step is the barrier, and DMA(s+2) is issued before a tile end's
 // epilogue stores, so the next wait never drains them (counted vmcnt).
-template <int BM, int BN, int WM, int WN, int NS = 2>
+template <int BM, int BN, int WM, int WN>
 struct Cfg2 {
   static constexpr int NW = WM * WN;
   static constexpr int NT = NW * 64;
   static constexpr int TM = BM / WM / 16;
   static constexpr int TN = BN / WN / 16;
   static constexpr int STAGE_BYTES = (BM + BN) * BK * 2;
-  static constexpr int LDS = NS * STAGE_BYTES;   // NS-buffer ring: DMA lead of NS-1 K-steps
+  static constexpr int LDS = 2 * STAGE_BYTES;   // two-buffer ring: DMA lead of one K-step
   static constexpr int LA = BM / 8 / NW;
   static constexpr int LB = BN / 8 / NW;
   static_assert(BM % (8 * NW) == 0 && BN % (8 * NW) == 0, "rows must split evenly over waves");
@@ -34,12 +34,11 @@ struct Cfg2 {
 
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
 
-template <bool BF, int EPI, int BM, int BN, int WM, int WN, bool DEFER, int NS>
+template <bool BF, int EPI, int BM, int BN, int WM, int WN>
 __global__ __launch_bounds__(WM * WN * 64, 1) void gemm2_kernel(GemmArgs ga) {
-  using C = Cfg2<BM, BN, WM, WN, NS>;
+  using C = Cfg2<BM, BN, WM, WN>;
   GemmArgs g = ga;   // varlen: the device-resident row count (the grid was sized for ga.M)
   if (g.m_dev) g.M = __builtin_amdgcn_readfirstlane(*g.m_dev);
-  static_assert(NS == 2 || NS == 3, "ring of 2 or 3 buffers");
   constexpr int L = C::LA + C::LB;   // vmcnt units (DMA instructions) per K-step
   constexpr int TM = C::TM, TN = C::TN;
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
@@ -48,7 +47,7 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void gemm2_kernel(GemmArgs ga) {
   const int wm = wid / WN, wn = wid % WN;
   const int ntn = (g.N + BN - 1) / BN, ntm = (g.M + BM - 1) / BM;
   const int ntiles = ntn * ntm, G = gridDim.x;
-  const TileWalk tw = tile_walk(ntiles, G, g.band != 0);
+  const TileWalk tw = tile_walk(ntiles, G);
   if (tw.count <= 0) return;   // varlen: fewer live tiles than the grid
   const int n_my = tw.count;
   const int nk = g.K / BK;
@@ -61,7 +60,6 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void gemm2_kernel(GemmArgs ga) {
       tm = t % ntm;
       tn = t / ntm;
     } else {
-      const int GM = g.gm > 0 ? g.gm : 4;
       const int group = t / (GM * ntn);
       const int first_m = group * GM;
       const int gsz = min(GM, ntm - first_m);
@@ -134,8 +132,7 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void gemm2_kernel(GemmArgs ga) {
 
   dma_next(0);
   if (S > 1) dma_next(1);
-  if (NS == 3 && S > 2) dma_next(2);
-  if (S >= NS) wait_vmcnt<L * (NS - 1)>();   // DMA(0) retired, the younger ones in flight
+  if (S >= 2) wait_vmcnt<L>();   // DMA(0) retired, DMA(1) in flight
   else wait_vmcnt<0>();
   lds_barrier();
   u32x4 a0[TM], b0[TN], a1[TM], b1[TN];
@@ -144,25 +141,8 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void gemm2_kernel(GemmArgs ga) {
   constexpr int E0 = epi_min_stores<EPI, TM, TN>();
   constexpr int E = E0 > 63 ? 63 : E0;
   const bool vec_epi = (g.N % 4) == 0 && (g.ldo % 4) == 0 && !(g.debug & 1);
-  // DEFER (STORE / GELU, 16-B store path only): a tile's output is converted to packed
-  // 16-bit units at its end (bias, quick-GELU, pair swap) but stored one 1-KiB wave-store per
-  // K-step of the NEXT tile, so the per-CU store data path (~16 B/clk) drains beside that
-  // tile's MFMAs instead of in a burst the whole chip waits for.
-  constexpr int NU = DEFER ? TM * TN / 2 : 1;
-  static_assert(!DEFER || ((EPI == EPI_STORE || EPI == EPI_GELU) && TN % 2 == 0), "DEFER: 16-B store epilogues");
-  u32x4 pend[NU];
-  int pm0 = 0, pn0 = 0;
-  bool have = false, stored = false;
-  auto store_unit = [&](int u) {   // u: compile-time after unrolling
-    const int mb = u / (TN / 2), nb = (u % (TN / 2)) * 2, q = lane >> 4;
-    const int m = pm0 + wm * (BM / WM) + (lane & 15) + mb * 16;
-    const int col = pn0 + wn * (BN / WN) + (q & 1) * 16 + (q >> 1) * 8 + nb * 16;
-    const auto ob = buf_rsrc((const u16*)g.out + (int64_t)pm0 * g.ldo);
-    const uint32_t off = (m < g.M && col < g.N) ? (uint32_t)(((m - pm0) * g.ldo + col) * 2) : BUF_OOB;
-    __builtin_amdgcn_raw_buffer_store_b128(pend[u], ob, off, 0, 0);
-  };
   int s = 0;     // K-step of the ring (all tiles of this workgroup)
-  int cur = 0;   // its LDS buffer, s % NS
+  int cur = 0;   // its LDS buffer, s % 2
   for (int ti = 0; ti < n_my; ++ti) {
     int m0, n0;
     coords(ti, m0, n0);
@@ -173,94 +153,35 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void gemm2_kernel(GemmArgs ga) {
     for (int kt = 0; kt < nk; ++kt, ++s) {
       read_frags(smem + cur * C::STAGE_BYTES, 1, a1, b1);
       mma(a0, b0);
-      const int nxt = cur + 1 == NS ? 0 : cur + 1;
+      const int nxt = cur ^ 1;
       if (s + 1 < S) {
-        // DMA(s+1) retired -- younger: DMA(s+2) when NS = 3, and the stores issued after the
-        // DMAs of the previous step (a tile end's epilogue, or one deferred unit) -- kk1
-        // fragments of s landed, and after the barrier no wave reads buffer `cur` any more
-        const bool more = NS == 3 && s + 2 < S;
-        if constexpr (DEFER) {
-          if (stored) { if (more) wait_vmcnt<L * (NS - 2) + 1>(); else wait_vmcnt<1>(); }
-          else { if (more) wait_vmcnt<L * (NS - 2)>(); else wait_vmcnt<0>(); }
-        } else {
-          // the previous tile's E epilogue stores were issued after DMA(s+NS-1) of its last step:
-          // with NS = 3 they sit between DMA(s+1) and DMA(s+2) at kt = 1 too, so they need not
-          // drain until kt = 2 -- three K-steps for the burst instead of one
-          if (kt == 0 && ti > 0 && vec_epi) { if (more) wait_vmcnt<(L * (NS - 2) + E > 63 ? 63 : L * (NS - 2) + E)>(); else wait_vmcnt<E>(); }
-          else if (NS == 3 && kt == 1 && ti > 0 && vec_epi) { if (more) wait_vmcnt<(L + E > 63 ? 63 : L + E)>(); else wait_vmcnt<E>(); }
-          else { if (more) wait_vmcnt<L * (NS - 2)>(); else wait_vmcnt<0>(); }
-        }
+        // DMA(s+1) retired -- kk1 fragments of s landed, and after the barrier no wave reads
+        // buffer `cur` any more. The previous tile's E epilogue stores were issued after DMA(s+1)
+        // of its last step, so at kt = 0 they may stay in flight.
+        if (kt == 0 && ti > 0 && vec_epi) wait_vmcnt<E>();
+        else wait_vmcnt<0>();
         lds_barrier();
-        if (s + NS < S) dma_next(cur);
+        if (s + 2 < S) dma_next(cur);
         read_frags(smem + nxt * C::STAGE_BYTES, 0, a0, b0);
       }
       mma(a1, b1);
       cur = nxt;
-      if constexpr (DEFER) {
-        stored = have && kt < NU;
-        if (stored) {
-#pragma unroll
-          for (int u = 0; u < NU; ++u)
-            if (u == kt) store_unit(u);
-        }
-      }
     }
     if (g.debug & 1) {
 #pragma unroll
       for (int mb = 0; mb < TM; ++mb)
 #pragma unroll
         for (int nb = 0; nb < TN; ++nb) asm volatile("" ::"v"(acc[mb][nb]));
-    } else if constexpr (DEFER) {
-      if (have && nk < NU) {   // short K: flush the units the loop did not reach
-#pragma unroll
-        for (int u = 0; u < NU; ++u)
-          if (u >= nk) store_unit(u);
-        stored = false;
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // keep the counted waits exact
-      }
-      const int q = lane >> 4;
-#pragma unroll
-      for (int mb = 0; mb < TM; ++mb) {
-#pragma unroll
-        for (int nb = 0; nb < TN; nb += 2) {
-          uint32_t w[2][2];
-#pragma unroll
-          for (int h = 0; h < 2; ++h) {
-            const int n = n0 + wn * (BN / WN) + (nb + h) * 16 + q * 4;
-            const float4 c = (g.bias && n < g.N) ? *(const float4*)(g.bias + n) : make_float4(0.f, 0.f, 0.f, 0.f);
-            float v[4] = {acc[mb][nb + h][0] + c.x, acc[mb][nb + h][1] + c.y, acc[mb][nb + h][2] + c.z,
-                          acc[mb][nb + h][3] + c.w};
-            if constexpr (EPI == EPI_GELU) {
-#pragma unroll
-              for (int j = 0; j < 4; ++j) v[j] = quick_gelu(v[j]);
-            }
-            w[h][0] = pack2<BF>(v[0], v[1]);
-            w[h][1] = pack2<BF>(v[2], v[3]);
-          }
-          const auto rx = __builtin_amdgcn_permlane16_swap(w[0][0], w[1][0], false, false);
-          const auto ry = __builtin_amdgcn_permlane16_swap(w[0][1], w[1][1], false, false);
-          pend[mb * (TN / 2) + nb / 2] = u32x4{rx[0], ry[0], rx[1], ry[1]};
-        }
-      }
-      pm0 = m0;
-      pn0 = n0;
-      have = true;
     } else {
       epilogue<BF, EPI, BM, BN, WM, WN, 2>(g, acc, m0, n0, wm, wn, lane);
     }
   }
-  if constexpr (DEFER) {
-    if (have) {
-#pragma unroll
-      for (int u = 0; u < NU; ++u) store_unit(u);
-    }
-  }
 }
 
-template <bool BF, int EPI, int BM, int BN, int WM, int WN, bool DEFER = false, int NS = 2>
+template <bool BF, int EPI, int BM, int BN, int WM, int WN>
 hipError_t launch_cfg2(const GemmArgs& g, hipStream_t s) {
-  using C = Cfg2<BM, BN, WM, WN, NS>;
-  auto kern = gemm2_kernel<BF, EPI, BM, BN, WM, WN, DEFER, NS>;
+  using C = Cfg2<BM, BN, WM, WN>;
+  auto kern = gemm2_kernel<BF, EPI, BM, BN, WM, WN>;
   static unsigned dev_done = 0;
   int dev = 0;
   (void)hipGetDevice(&dev);
@@ -276,44 +197,20 @@ hipError_t launch_cfg2(const GemmArgs& g, hipStream_t s) {
     (void)hipGetLastError();
   }
   const int tiles = ((g.N + BN - 1) / BN) * ((g.M + BM - 1) / BM);
-  const int nwg = (g.debug & 4) ? tiles : std::min(tiles, std::max(1, cus * grid_pct() / 100));   // <= one per CU
-  GemmArgs ga = g;
-  ga.band = gemm_band();
-  ga.gm = gemm_gm();
-  kern<<<dim3(nwg), dim3(C::NT), C::LDS, s>>>(ga);
+  const int nwg = (g.debug & 4) ? tiles : std::min(tiles, cus);   // <= one per CU
+  kern<<<dim3(nwg), dim3(C::NT), C::LDS, s>>>(g);
   return hipGetLastError();
 }
 
 
 template <bool BF, int EPI>
 hipError_t by_id(int id, const GemmArgs& g, hipStream_t s) {
-  if constexpr (epi_ln(EPI)) {   // LayerNorm-folded epilogues: TN <= 4 tiles only
-    switch (id) {
-      case 16: return launch_cfg2<BF, EPI, 256, 128, 4, 2>(g, s);
-      case 17: return launch_cfg2<BF, EPI, 192, 256, 2, 4>(g, s);
-      case 18: return launch_cfg2<BF, EPI, 128, 256, 2, 4>(g, s);
-      default: return hipErrorInvalidValue;
-    }
-  } else {
   switch (id) {
-    case 11: return launch_cfg2<BF, EPI, 256, 256, 2, 2>(g, s);
-    case 12: return launch_cfg2<BF, EPI, 256, 128, 2, 2>(g, s);
-    case 13: return launch_cfg2<BF, EPI, 128, 256, 2, 2>(g, s);
-    case 14: return launch_cfg2<BF, EPI, 256, 256, 4, 2>(g, s);
-    case 15: return launch_cfg2<BF, EPI, 256, 192, 4, 2>(g, s);
-    case 16: return launch_cfg2<BF, EPI, 256, 128, 4, 2>(g, s);
-    case 17: return launch_cfg2<BF, EPI, 192, 256, 2, 4>(g, s);
-    case 18: return launch_cfg2<BF, EPI, 128, 256, 2, 4>(g, s);
-    case 19: case 20: {   // deferred-store variants of 16 / 18 (16-B store epilogues only)
-      constexpr bool D = EPI == EPI_STORE || EPI == EPI_GELU;
-      const bool wide = (g.N % 8) == 0 && (g.ldo % 8) == 0 && ((uintptr_t)g.out & 15) == 0;
-      if (id == 19) return D && wide ? launch_cfg2<BF, EPI, 256, 128, 4, 2, D>(g, s) : launch_cfg2<BF, EPI, 256, 128, 4, 2>(g, s);
-      return D && wide ? launch_cfg2<BF, EPI, 128, 256, 2, 4, D>(g, s) : launch_cfg2<BF, EPI, 128, 256, 2, 4>(g, s);
-    }
-    case 21: return launch_cfg2<BF, EPI, 256, 128, 4, 2, false, 3>(g, s);   // 3-buffer rings: 144 KiB
-    case 22: return launch_cfg2<BF, EPI, 128, 256, 2, 4, false, 3>(g, s);
+    case 8: return launch_cfg2<BF, EPI, 256, 192, 4, 2>(g, s);
+    case 9: return launch_cfg2<BF, EPI, 256, 128, 4, 2>(g, s);
+    case 10: return launch_cfg2<BF, EPI, 192, 256, 2, 4>(g, s);
+    case 11: return launch_cfg2<BF, EPI, 128, 256, 2, 4>(g, s);
     default: return hipErrorInvalidValue;
-  }
   }
 }
 template <bool BF>
@@ -325,8 +222,6 @@ hipError_t by_epi(int epi, int id, const GemmArgs& g, hipStream_t s) {
     case EPI_PATCH: return by_id<BF, EPI_PATCH>(id, g, s);
     case EPI_SCORE: return by_id<BF, EPI_SCORE>(id, g, s);
     case EPI_FILTER: return by_id<BF, EPI_FILTER>(id, g, s);
-    case EPI_STORE_LN: return by_id<BF, EPI_STORE_LN>(id, g, s);
-    case EPI_GELU_LN: return by_id<BF, EPI_GELU_LN>(id, g, s);
     default: return hipErrorInvalidValue;
   }
 }

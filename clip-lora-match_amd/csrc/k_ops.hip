@@ -233,19 +233,6 @@ __global__ __launch_bounds__(256) void ln4_kernel(LnArgs aa) {
 template <bool BF>
 hipError_t ln_dispatch(const LnArgs& a, hipStream_t s) {
   dim3 grid((a.M + 3) / 4), block(256);
-  // ln4_kernel rows per wave: 2 (default) or 4 ($CLM_LN_ROWS=4, A/B: twice the loads in flight
-  // per wave at the same occupancy)
-  static const int rows = (getenv("CLM_LN_ROWS") && atoi(getenv("CLM_LN_ROWS")) == 4) ? 4 : 2;
-  if (rows == 4 && a.d >= 256 && a.d <= 1024 && a.d % 256 == 0) {
-    dim3 grid4((a.M + 15) / 16);
-    switch (a.d) {
-      case 256: ln4_kernel<BF, 1, 4><<<grid4, block, 0, s>>>(a); break;
-      case 512: ln4_kernel<BF, 2, 4><<<grid4, block, 0, s>>>(a); break;
-      case 768: ln4_kernel<BF, 3, 4><<<grid4, block, 0, s>>>(a); break;
-      case 1024: ln4_kernel<BF, 4, 4><<<grid4, block, 0, s>>>(a); break;
-    }
-    return hipGetLastError();
-  }
   dim3 grid2((a.M + 7) / 8);   // ln4_kernel: 2 rows per wave
   switch (a.d) {
     case 128: ln_kernel<BF, 1><<<grid, block, 0, s>>>(a); break;
@@ -659,35 +646,6 @@ __global__ __launch_bounds__(256) void fuse_rows_kernel(const float* a, float wa
   }
 }
 
-// LayerNorm statistics from per-row 32-column moments (mean, M2), combined in chunk order (Chan
-// et al.): one thread per row, 64-thread blocks (enough blocks to spread a 12 800-row launch over
-// the chip), the row's chunks loaded before they are combined.
-template <int CH>
-__global__ __launch_bounds__(64) void ln_finalize_kernel(const float2* stats, int M, float eps, float2* out) {
-  const int m = blockIdx.x * 64 + threadIdx.x;
-  if (m >= M) return;
-  const float4* p = (const float4*)(stats + (int64_t)m * CH);
-  float2 c[CH];
-#pragma unroll
-  for (int i = 0; i < CH / 2; ++i) {
-    const float4 v = p[i];
-    c[2 * i] = make_float2(v.x, v.y);
-    c[2 * i + 1] = make_float2(v.z, v.w);
-  }
-  float n = 0.f, mean = 0.f, m2 = 0.f;
-#pragma unroll
-  for (int i = 0; i < CH; ++i) {
-    const float2 v = c[i];
-    const float nab = n + 32.f, d = v.x - mean;
-    mean += d * (32.f / nab);
-    m2 += v.y + d * d * (n * 32.f / nab);
-    n = nab;
-  }
-  const float var = m2 / n;   // biased variance, as nn.LayerNorm
-  const float rstd = 1.0f / sqrtf(var + eps);
-  out[m] = make_float2(rstd, -rstd * mean);
-}
-
 __global__ __launch_bounds__(256) void f32_to_f16_kernel(const float* src, int64_t total, u16* dst) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
        i += (int64_t)gridDim.x * blockDim.x)
@@ -700,23 +658,6 @@ hipError_t layernorm(bool bf16, const LnArgs& a, hipStream_t s) {
   if (a.M <= 0) return hipSuccess;
   if (a.r_ext > 64 || a.r_pad > 64) return hipErrorInvalidValue;
   return bf16 ? ln_dispatch<true>(a, s) : ln_dispatch<false>(a, s);
-}
-
-hipError_t ln_finalize(const float2* stats, int chunks, int M, float eps, float2* out, hipStream_t s) {
-  if (M <= 0) return hipSuccess;
-  const unsigned grid = (unsigned)((M + 63) / 64);
-  switch (chunks) {   // d = 128 .. 1024 in steps of 128
-    case 4: ln_finalize_kernel<4><<<grid, 64, 0, s>>>(stats, M, eps, out); break;
-    case 8: ln_finalize_kernel<8><<<grid, 64, 0, s>>>(stats, M, eps, out); break;
-    case 12: ln_finalize_kernel<12><<<grid, 64, 0, s>>>(stats, M, eps, out); break;
-    case 16: ln_finalize_kernel<16><<<grid, 64, 0, s>>>(stats, M, eps, out); break;
-    case 20: ln_finalize_kernel<20><<<grid, 64, 0, s>>>(stats, M, eps, out); break;
-    case 24: ln_finalize_kernel<24><<<grid, 64, 0, s>>>(stats, M, eps, out); break;
-    case 28: ln_finalize_kernel<28><<<grid, 64, 0, s>>>(stats, M, eps, out); break;
-    case 32: ln_finalize_kernel<32><<<grid, 64, 0, s>>>(stats, M, eps, out); break;
-    default: return hipErrorInvalidValue;
-  }
-  return hipGetLastError();
 }
 
 hipError_t lora_down(bool bf16, u16* X, int64_t ldx, int M, int K, const float* A, int r_ext, int r_pad,

@@ -13,14 +13,11 @@ enum Epi {
   EPI_RESID = 2,  // outf[m,n] += acc + bias[n]            (fp32 residual stream)
   EPI_PATCH = 3,  // outf[b*(G+1)+1+p, n] = acc + aux[(1+p)*aux_ld + n], m = b*G+p
   EPI_SCORE = 4,  // outf[m,n] = acc * rscale[m] * cscale[n]  (cosine scores)
-  EPI_FILTER = 5,  // s = acc*rscale[m]*cscale[n]; if s >= theta[m]: append (s, base+n) to row m's
+  EPI_FILTER = 5   // s = acc*rscale[m]*cscale[n]; if s >= theta[m]: append (s, base+n) to row m's
                    // candidate list (atomic slot in cnt[m], capacity cap)
-  EPI_STORE_LN = 6,  // EPI_STORE / EPI_GELU with the LayerNorm folded in (GemmArgs::lnstat / cvec):
-  EPI_GELU_LN = 7    // out16[m,n] = [gelu](acc * lnstat[m].x + lnstat[m].y * cvec[n] + bias[n])
 };
-constexpr bool epi_stores16(int e) { return e == EPI_STORE || e == EPI_GELU || e == EPI_STORE_LN || e == EPI_GELU_LN; }
-constexpr bool epi_gelu(int e) { return e == EPI_GELU || e == EPI_GELU_LN; }
-constexpr bool epi_ln(int e) { return e == EPI_STORE_LN || e == EPI_GELU_LN; }
+constexpr bool epi_stores16(int e) { return e == EPI_STORE || e == EPI_GELU; }
+constexpr bool epi_gelu(int e) { return e == EPI_GELU; }
 
 struct GemmArgs {
   const u16* A; int64_t lda;
@@ -32,17 +29,6 @@ struct GemmArgs {
   const float* rscale; const float* cscale;
   // EPI_FILTER
   const float* theta; int64_t theta_ld; int* cnt; float* cand_s; int64_t* cand_i; int cap; int64_t base;
-  // LayerNorm folding (capi.cpp run_layers, merged-LoRA mode):
-  //  producer (EPI_RESID with stats != null, N % 32 == 0): also writes hb[m, n] = 16-bit copy
-  //    of the new residual row, and per row and 32-column chunk j the moments (mean, M2) of
-  //    its 32 values to stats[m * (N / 32) + j] -- chunks, not tiles, so the statistics do not
-  //    depend on the tile configuration (batch invariance);
-  //  consumer (EPI_STORE_LN / EPI_GELU_LN): acc was computed on the 16-bit
-  //    residual against W' = W diag(gamma); out = acc * lnstat[m].x + lnstat[m].y * cvec[n] +
-  //    bias[n] (x = rstd, y = -rstd * mean, cvec = row sums of W', bias = b + W beta), i.e.
-  //    Linear(LayerNorm(h)) without materialising LayerNorm(h).
-  u16* hb; int64_t ldhb; float2* stats;
-  const float2* lnstat; const float* cvec;
   int m_fastest;   // tile order: 1 = consecutive workgroups walk M (share one W tile)
   // split-K (gemm_kernel configs only, EPI_SCORE as the fp32 partial store): ksplit > 1 cuts K
   // into ksplit equal slices; slice s of every tile writes out + s * split_stride
@@ -50,8 +36,6 @@ struct GemmArgs {
   // varlen rows (packed text tower): if set, the row count is *m_dev (device-resident, <= M, which
   // sizes the grid), so a captured graph replays with data-dependent row counts
   const int* m_dev;
-  int band;        // persistent tile walk in one band per XCD group (gemm_common.hpp tile_walk); set by the launcher
-  int gm;          // grouped raster: row panels per group (0 = 4); set by the launcher ($CLM_GEMM_GM)
   int debug;       // diagnostics only: 1 = skip the epilogue (accumulators kept live), 2 = drop its
                    // stores, 4 = one tile per workgroup (non-persistent grid)
 };
@@ -63,7 +47,9 @@ hipError_t gemm(bool bf16, int epi, const GemmArgs& g, hipStream_t s);
 hipError_t gemm_splitk_resid(bool bf16, const GemmArgs& g, int slices, float* ws, hipStream_t s);
 // fp32 workspace bytes gemm_splitk_resid needs
 inline size_t gemm_splitk_ws_bytes(int M, int N, int slices) { return (size_t)slices * M * N * 4; }
-// explicit tile configuration (config < 0: heuristic); configs: k_gemm.hip launch_id
+// explicit tile configuration (config < 0: heuristic); configs: k_gemm.hip launch_id.
+// GEMM_CFG_SPLITK: the 64 x 128 tile, for few-row GEMMs (the pooled last layer)
+constexpr int GEMM_CFG_SPLITK = 2;
 hipError_t gemm_cfg(bool bf16, int epi, int config, const GemmArgs& g, hipStream_t s);
 int gemm_num_configs();
 // host-side hint for the tile heuristic of the calling thread: true while two towers are being
@@ -95,10 +81,6 @@ struct LnArgs {
   const int* m_dev; const int* rowmap;
 };
 hipError_t layernorm(bool bf16, const LnArgs& a, hipStream_t s);
-// per-row LayerNorm statistics from a stats-producing GEMM's 32-column moments (Chan's parallel
-// combination in chunk order, deterministic): out[m] = (rstd, -rstd * mean), var + eps under the
-// square root (TF/models/clip/modeling_clip.py:358,360 nn.LayerNorm, eps 1e-5)
-hipError_t ln_finalize(const float2* stats, int chunks, int M, float eps, float2* out, hipStream_t s);
 
 // y[:, K : K+r_pad) = (X[:, :K] . A^T) for LoRA K-extension of a GEMM whose input
 // is not a LayerNorm output (out_proj after attention, fc2 after GELU).

@@ -243,29 +243,6 @@ def test_last_layer_pruning_exact(preset, mode):
         assert np.max(np.abs(a - b)) <= 1e-6, f"pruned vs every-row: {np.max(np.abs(a - b)):.3e}"
 
 
-@pytest.mark.parametrize("dtype", ["float16", "bfloat16"])
-def test_ln_fold_matches_layernorm_kernels(dtype, monkeypatch):
-    """LayerNorm folded into qkv / fc1 ($CLM_LN_FOLD=1, merged mode) vs the LayerNorm kernels
-    (the default): the same model within the dtype's score bar, both vs the golden; the
-    folded path is deterministic and batch-invariant (its row moments come in fixed 32-column
-    chunks, independent of the GEMM tile configuration)."""
-    g = golden("enc_b32_lora.npz")
-    outs = {}
-    for fold in ("1", "0"):
-        monkeypatch.setenv("CLM_LN_FOLD", fold)
-        m, cfg, _, _ = _model("ViT-B/32", dtype, max_batch=16)
-        imgs = torch.from_numpy(syn.images_u8(int(g["n_img"]), cfg.image_size, int(g["img_seed"]))).cuda()
-        ids = torch.from_numpy(g["ids"]).cuda()
-        gi, gt = m.encode_pixels(imgs), m.encode_ids(ids)
-        if fold == "1":
-            assert torch.equal(gi, m.encode_pixels(imgs)) and torch.equal(gt, m.encode_ids(ids))
-            assert torch.equal(m.encode_pixels(imgs[1:3]), gi[1:3]) and torch.equal(m.encode_ids(ids[2:]), gt[2:])
-        outs[fold] = (gi.cpu().numpy(), gt.cpu().numpy())
-        _check(outs[fold][0], outs[fold][1], g["emb_img"], g["emb_txt"], dtype)
-        m.close()
-    _check(outs["1"][0], outs["1"][1], outs["0"][0], outs["0"][1], dtype)
-
-
 @pytest.mark.parametrize("preset,dtype,mode", [("tiny", "float16", "merged"), ("tiny", "bfloat16", "unmerged"),
                                                ("ViT-B/32", "bfloat16", "merged"), ("ViT-B/32", "float16", "merged"),
                                                ("ViT-B/32", "bfloat16", "unmerged")])

@@ -21,7 +21,7 @@ def _gemm(dtype, epi, cfg, A, W, out, bias=None, rs=None, cs=None):
 
 
 @pytest.mark.parametrize("dtype", ["bfloat16", "float16"])
-@pytest.mark.parametrize("cfg", list(range(25)) + [-1])
+@pytest.mark.parametrize("cfg", list(range(12)) + [-1])
 @pytest.mark.parametrize("shape", [(333, 200, 128), (1000, 768, 768), (77, 2304, 512), (97, 100, 64), (65, 50, 128)])
 def test_gemm_epilogues_vs_torch(dtype, cfg, shape):
     M, N, K = shape

@@ -153,3 +153,10 @@ def test_c_abi_under_host_sanitizers():
     p = subprocess.run([_host_check()], capture_output=True, text=True, timeout=300)
     assert p.returncode == 0, p.stdout + p.stderr
     assert "argument checks (no HIP device), 0 failure(s)" in p.stdout
+
+
+def test_gemm_config_table_matches_the_test_matrix():
+    """every tile config is reachable by the picker (k_gemm.hip pick_config); the GPU test matrix
+    (test_gpu_kernels.py) covers exactly these ids"""
+    from clip_lora_match_amd import _capi as C
+    assert C.lib().clm_gemm_num_configs() == 12
