@@ -728,6 +728,10 @@ def main():
             "avg_launch_us": round(gemm_ms / gemm_n * 1e3, 2),
             "launches_per_step": gemm_n // nprof,
             "kernel_ms_per_step": {k: round(v[0] / nprof, 4) for k, v in prof.items()},
+            "mode": "per-kernel durations from a separate profiled pass (HIP events on the launch stream around "
+                    "every GEMM, towers one after the other so no two kernels share the chip); the timed step "
+                    "runs both towers concurrently, see step_frac",
+            "step_frac": round(step_flops / (ms_step * 1e-3) / 1e12 / MFMA_PEAK_TFLOPS, 4),
         },
     }
     if world > 1:

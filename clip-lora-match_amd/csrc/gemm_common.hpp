@@ -99,10 +99,33 @@ __device__ __forceinline__ void epilogue_scalar(const GemmArgs& g, const f32x4 (
   }
 }
 
-// Epilogue of one BM x BN tile from the accumulators.
-template <bool BF, int EPI, int BM, int BN, int WM, int WN, int STAGES>
+// Residual prefetch (EPI_RESID in gemm_kernel): the fp32 residual values of the first P row-blocks
+// a lane's epilogue adds to, loaded into registers while the tile's last K-step still computes --
+// that part of the read-modify-write's reads overlaps the main loop instead of following it. Same
+// buffer offsets as the epilogue (out-of-range lanes read BUF_OOB: zeros, never stored).
+template <int BM, int BN, int WM, int WN, int P>
+__device__ __forceinline__ void resid_prefetch(const GemmArgs& g, int m0, int n0, int wm, int wn, int lane,
+                                               u32x4 (&h)[P][BN / WN / 16]) {
+  const auto ob = buf_rsrc((const float*)g.out + (int64_t)m0 * g.ldo);
+  const int wrow = m0 + wm * (BM / WM) + (lane & 15);
+  const int wcol = n0 + wn * (BN / WN) + (lane >> 4) * 4;
+#pragma unroll
+  for (int mb = 0; mb < P; ++mb)
+#pragma unroll
+    for (int nb = 0; nb < BN / WN / 16; ++nb) {
+      const int m = wrow + mb * 16, n = wcol + nb * 16;
+      const uint32_t oo = (m < g.M && n < g.N) ? (uint32_t)(((int64_t)(m - m0) * g.ldo + n) * 4) : BUF_OOB;
+      h[mb][nb] = __builtin_amdgcn_raw_buffer_load_b128(ob, oo, 0, 0);
+    }
+}
+
+// Epilogue of one BM x BN tile from the accumulators. PRE > 0 (EPI_RESID only): the residual
+// values of row-blocks 0 .. PRE-1 are already in hpre (resid_prefetch).
+template <bool BF, int EPI, int BM, int BN, int WM, int WN, int STAGES, int PRE = 0>
 __device__ __forceinline__ void epilogue(const GemmArgs& g, const f32x4 (&acc)[BM / WM / 16][BN / WN / 16], int m0,
-                                         int n0, int wm, int wn, int lane, int64_t out_off = 0) {
+                                         int n0, int wm, int wn, int lane, int64_t out_off = 0,
+                                         const u32x4 (*hpre)[BN / WN / 16] = nullptr) {
+  static_assert(PRE == 0 || EPI == EPI_RESID, "residual prefetch: RESID epilogue only");
   using C = Cfg<BM, BN, WM, WN, STAGES>;
   // lane owns C[m, n..n+3], m = wrow + 16*mb, n = wcol + 16*nb.
   // Every global load of the epilogue (bias / cscale / row scales, residual, pos rows) is
@@ -120,7 +143,8 @@ __device__ __forceinline__ void epilogue(const GemmArgs& g, const f32x4 (&acc)[B
   }
   // per-column vectors, loaded once per nb (they do not depend on the row); the RESID/PATCH
   // path with TN > 4 loads them per row-block instead (VGPR budget, see below)
-  constexpr bool HOIST = !(EPI == EPI_RESID || EPI == EPI_PATCH) || C::TN <= 4;
+  // (PRE: the first blocks load nothing, so the bias vectors are hoisted too)
+  constexpr bool HOIST = !(EPI == EPI_RESID || EPI == EPI_PATCH) || C::TN <= 4 || PRE > 0;
   float4 cv[C::TN];
 #pragma unroll
   for (int nb = 0; nb < C::TN; ++nb) {
@@ -211,13 +235,22 @@ __device__ __forceinline__ void epilogue(const GemmArgs& g, const f32x4 (&acc)[B
       }
     };
     // pipelining holds 2 * TN float4 of loaded rows; where that would cost a wave per SIMD
-    // (TN > 4, or PATCH's extra address VALU) one block at a time is loaded, then stored
+    // (TN > 4, or PATCH's extra address VALU) one block at a time is loaded, then stored.
+    // With P = PRE prefetched blocks, block P is loaded before the first store and the
+    // pipelining (or the block-by-block loads) takes over from there.
+    constexpr int P = EPI == EPI_RESID ? PRE : 0;
     constexpr bool PIPE = EPI == EPI_RESID && C::TN <= 4;
     u32x4 hc[C::TN], hn[C::TN];
-    load_blk(0, hc);
+    if constexpr (P > 0) {
+#pragma unroll
+      for (int nb = 0; nb < C::TN; ++nb) hc[nb] = hpre[0][nb];
+      if (P < C::TM) load_blk(P, hn);
+    } else {
+      load_blk(0, hc);
+    }
 #pragma unroll
     for (int mb = 0; mb < C::TM; ++mb) {
-      if (PIPE && mb + 1 < C::TM) load_blk(mb + 1, hn);
+      if (PIPE && mb >= P && mb + 1 < C::TM) load_blk(mb + 1, hn);
 #pragma unroll
       for (int nb = 0; nb < C::TN; ++nb) {
         uint32_t oo, ao;
@@ -231,7 +264,10 @@ __device__ __forceinline__ void epilogue(const GemmArgs& g, const f32x4 (&acc)[B
             u32x4{__float_as_uint(r0), __float_as_uint(r1), __float_as_uint(r2), __float_as_uint(r3)}, ob, oo, 0, 0);
       }
       if (mb + 1 < C::TM) {
-        if constexpr (PIPE) {
+        if (mb + 1 < P) {
+#pragma unroll
+          for (int nb = 0; nb < C::TN; ++nb) hc[nb] = hpre[(mb + 1) < P ? mb + 1 : 0][nb];
+        } else if (PIPE || mb + 1 == P) {
 #pragma unroll
           for (int nb = 0; nb < C::TN; ++nb) hc[nb] = hn[nb];
         } else {

@@ -129,14 +129,30 @@ __global__ __launch_bounds__(WM * WN * 64, (Cfg<BM, BN, WM, WN, STAGES>::WAVES_P
   int c_i = 0, c_kt = 0, m0, n0, k0;
   coords(0, m0, n0, k0);
   int since_end = STAGES;   // K-steps since the last tile end
+  // residual prefetch (RESID, 2-stage ring): the first PB row-blocks of the residual tile,
+  // issued right after the DMA of a tile's last K-step, so their reads land while that K-step
+  // computes (resid_prefetch). Only the 128 x 192 tile (TN = 6: the towers' concurrent RESID
+  // GEMMs) takes it, one row-block (24 VGPRs + the hoisted bias, no spill): +1.3 % pairs/s in the
+  // pair step; on the TN = 4 tiles it measured neutral (192 x 128) or slower (160 x 128, -8 %)
+  // (profiles/r03_v6_resid_prefetch_*)
+  constexpr int PB = (EPI == EPI_RESID && STAGES == 2 && C::TN == 6) ? 1 : 0;
+  constexpr bool PRE = PB > 0;
+  constexpr int XP = PB * C::TN;   // prefetch loads: the youngest ops at the next wait
+  u32x4 hpre[PRE ? PB : 1][C::TN];
+  const bool pre_on = PRE && ks == 1 && nk >= 2 && vec_epi;
+  bool hp_pending = false;
   for (int s = 0; s < S; ++s) {
     // retire K-step s's DMA, leaving younger ones in flight: the STAGES-2 later K-steps' DMA
     // and, for STAGES-1 steps after a tile end, that epilogue's stores (the DMA of those steps
-    // was issued before the stores; the first DMA issued after them is waited STAGES steps on)
+    // was issued before the stores; the first DMA issued after them is waited STAGES steps on),
+    // or the residual prefetch issued after this step's DMA
     const bool more = s + STAGES - 2 < S;
     ++since_end;
     const bool pe = vec_epi && since_end <= STAGES - 1;
-    if (more) {
+    if (PRE && hp_pending) {   // STAGES == 2: only the XP prefetch loads are younger than DMA(s)
+      wait_vmcnt<XP>();
+      hp_pending = false;
+    } else if (more) {
       if (pe) wait_vmcnt<C::L * (STAGES - 2) + E>();
       else wait_vmcnt<C::L * (STAGES - 2)>();
     } else {
@@ -145,6 +161,12 @@ __global__ __launch_bounds__(WM * WN * 64, (Cfg<BM, BN, WM, WN, STAGES>::WAVES_P
     }
     lds_barrier();
     if (s + STAGES - 1 < S) stage_next((s + STAGES - 1) % STAGES);
+    if constexpr (PRE) {
+      if (pre_on && c_kt == nk - 2) {
+        resid_prefetch<BM, BN, WM, WN, PRE ? PB : 1>(g, m0, n0, wm, wn, lane, hpre);
+        hp_pending = true;
+      }
+    }
     const uint8_t* sa = smem + (s % STAGES) * C::STAGE_BYTES;
     const uint8_t* sb = sa + BM * 128;
 #pragma unroll
@@ -174,8 +196,13 @@ __global__ __launch_bounds__(WM * WN * 64, (Cfg<BM, BN, WM, WN, STAGES>::WAVES_P
 #pragma unroll
           for (int nb = 0; nb < C::TN; ++nb) asm volatile("" ::"v"(acc[mb][nb]));
       } else {
-        epilogue<BF, EPI, BM, BN, WM, WN, STAGES>(g, acc, m0, n0, wm, wn, lane,
-                                                  ks > 1 ? (int64_t)(k0 / (nk * BK)) * g.split_stride : 0);
+        if constexpr (PRE) {
+          if (pre_on) epilogue<BF, EPI, BM, BN, WM, WN, STAGES, PB>(g, acc, m0, n0, wm, wn, lane, 0, hpre);
+          else epilogue<BF, EPI, BM, BN, WM, WN, STAGES>(g, acc, m0, n0, wm, wn, lane, 0);
+        } else {
+          epilogue<BF, EPI, BM, BN, WM, WN, STAGES>(g, acc, m0, n0, wm, wn, lane,
+                                                    ks > 1 ? (int64_t)(k0 / (nk * BK)) * g.split_stride : 0);
+        }
       }
 #pragma unroll
       for (int i = 0; i < C::TM; ++i)
@@ -225,7 +252,7 @@ hipError_t launch_id(int id, const GemmArgs& g, hipStream_t s) {
   switch (id) {
     case 0: return launch_cfg<BF, EPI, 128, 128, 2, 2, 2>(g, s);
     case 1: return launch_cfg<BF, EPI, 256, 256, 4, 2, 2>(g, s);
-    case 2: return launch_cfg<BF, EPI, 64, 128, 1, 2, 3>(g, s);
+    case 2: return launch_cfg<BF, EPI, 128, 64, 4, 1, 3>(g, s);
     case 3: return launch_cfg<BF, EPI, 128, 192, 2, 2, 2>(g, s);
     case 4: return launch_cfg<BF, EPI, 192, 128, 2, 2, 2>(g, s);
     case 5: return launch_cfg<BF, EPI, 256, 128, 4, 2, 2>(g, s);
@@ -237,7 +264,7 @@ hipError_t launch_id(int id, const GemmArgs& g, hipStream_t s) {
 }
 
 constexpr int NCFG = 12;
-static_assert(GEMM_CFG_SPLITK == 2, "config 2 is the 64 x 128 tile");
+static_assert(GEMM_CFG_SPLITK == 2, "config 2 is the 128 x 64 tile");
 
 // Tile choice: a cost model per kernel family, time(cfg) ~ rounds(cfg) x round_cost(cfg),
 // rounds = ceil(tiles / resident workgroups), round_cost = BM*BN*(workgroups per CU) /

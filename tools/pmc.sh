@@ -8,12 +8,12 @@ cd "$(dirname "$0")/.."
 export TMPDIR=/tmp
 mkdir -p gpurun_out/pmc
 i=0
-for grp in "FETCH_SIZE" "WRITE_SIZE" "SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU_MFMA_MOPS_BF16 GRBM_GUI_ACTIVE" \
+for grp in "FETCH_SIZE" "WRITE_SIZE" "SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU_MFMA_MOPS_BF16 SQ_INSTS_VALU_MFMA_MOPS_F16 GRBM_GUI_ACTIVE" \
            "SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_WAVES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE" \
            "TCC_HIT_sum TCC_MISS_sum GRBM_GUI_ACTIVE"; do
   i=$((i+1))
   timeout -k 10 240 rocprofv3 --kernel-trace --pmc $grp --output-format csv -d gpurun_out/pmc/p$i -o run -- \
-    python3 bench.py --steps 2 --warmup 1 --no-search --no-cpu-baseline --no-l14 --no-parity-mode --no-varlen --sequential \
+    python3 bench.py --steps 2 --warmup 1 --no-search --no-cpu-baseline --no-l14 --no-parity-mode --no-varlen --no-index-build --no-unmerged --sequential \
     > gpurun_out/pmc/p$i.log 2>&1
   rc=$?; echo "pmc pass $i ($grp) rc=$rc"
   [ $rc -eq 0 ] || { tail -5 gpurun_out/pmc/p$i.log; exit $rc; }

@@ -7,7 +7,8 @@ gfx950 corrections (MI355X_MICROARCH.md §HBM, § Per-instruction cycle constant
   * SQ_VALU_MFMA_BUSY_CYCLES counts SIMD-cycles summed over the chip; GRBM_GUI_ACTIVE is summed
     over the 8 XCDs -> kernel cycles = GRBM_GUI_ACTIVE / 8, and
     mfma_busy_frac = MFMA_BUSY / (kernel cycles * 256 CUs * 4 SIMDs).
-  * SQ_INSTS_VALU_MFMA_MOPS_BF16 counts 512-FLOP units -> MFMA FLOPs = 512 * MOPS.
+  * SQ_INSTS_VALU_MFMA_MOPS_BF16 / _F16 count 512-FLOP units -> MFMA FLOPs = 512 * MOPS (both
+    collected: the headline runs fp16 operands).
   * l2_hit_rate = TCC_HIT_sum / (TCC_HIT_sum + TCC_MISS_sum) (the XCD L2s; a miss is served by
     the Infinity Cache or HBM).
 GEMM launches are labelled by their position in the sequential encode step (tools/pmc.sh runs
@@ -93,8 +94,8 @@ def main(src="gpurun_out/pmc", tag="r02"):
         if "SQ_VALU_MFMA_BUSY_CYCLES" in m and m.get("GRBM_GUI_ACTIVE"):
             o["mfma_busy_frac"] = m["SQ_VALU_MFMA_BUSY_CYCLES"] / (m["GRBM_GUI_ACTIVE"] / N_XCD * N_CU * SIMD_PER_CU)
             o["kernel_cycles"] = m["GRBM_GUI_ACTIVE"] / N_XCD
-        if "SQ_INSTS_VALU_MFMA_MOPS_BF16" in m:
-            o["mfma_flops"] = 512 * m["SQ_INSTS_VALU_MFMA_MOPS_BF16"]
+        if "SQ_INSTS_VALU_MFMA_MOPS_BF16" in m or "SQ_INSTS_VALU_MFMA_MOPS_F16" in m:
+            o["mfma_flops"] = 512 * (m.get("SQ_INSTS_VALU_MFMA_MOPS_BF16", 0.0) + m.get("SQ_INSTS_VALU_MFMA_MOPS_F16", 0.0))
         if "SQ_LDS_BANK_CONFLICT" in m and m.get("SQ_INSTS_LDS"):
             o["lds_bank_conflicts_per_lds_inst"] = m["SQ_LDS_BANK_CONFLICT"] / m["SQ_INSTS_LDS"]
         if m.get("TCC_HIT_sum") is not None and m.get("TCC_MISS_sum") is not None and m["TCC_HIT_sum"] + m["TCC_MISS_sum"]:
