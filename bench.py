@@ -82,6 +82,7 @@ def parse_args(argv=None):
     ap.add_argument("--no-index-build", action="store_true", help="skip the configs[2] index-build leg")
     ap.add_argument("--index-images", type=int, default=1_000_000, help="images of the configs[2] index build")
     ap.add_argument("--index-batch", type=int, default=512)
+    ap.add_argument("--no-persist", action="store_true", help="skip the search index shard save / load timing")
     ap.add_argument("--sequential", action="store_true", help="towers back to back on one stream, no graph")
     ap.add_argument("--split", type=int, default=0, help="sub-batches per tower in encode_pair (0 = library default)")
     return ap.parse_args(argv)
@@ -259,7 +260,36 @@ def _topk_ordered(s: torch.Tensor, i: torch.Tensor, k: int):
     return torch.gather(s, 1, o), torch.gather(i, 1, o)
 
 
-def search_leg(rows: int, queries: int, k: int, device, world: int = 1, rank: int = 0, keep_host: bool = False):
+def shard_roundtrip(idx, q, k) -> dict:
+    """The index persisted as a raw shard (CosineIndex.save_shard: fp16 rows + fp32 inverse norms,
+    streamed through a pinned buffer) and loaded back into HBM (load_shard), timed; the reloaded
+    index must answer the same queries bit for bit."""
+    import shutil
+    import tempfile
+    from clip_lora_match_amd.search import CosineIndex
+    d = tempfile.mkdtemp(prefix="clm_shard_")
+    try:
+        path = os.path.join(d, "index.clmidx")
+        s0, i0 = idx.search(q, k)
+        t0 = time.perf_counter()
+        idx.save_shard(path)
+        t1 = time.perf_counter()
+        re, _ = CosineIndex.load_shard(path, device=idx.device)
+        torch.cuda.synchronize()
+        t2 = time.perf_counter()
+        s1, i1 = re.search(q, k)
+        same = bool(torch.equal(s0, s1) and torch.equal(i0, i1))
+        nbytes = os.path.getsize(path)
+        re.close()
+    finally:
+        shutil.rmtree(d, ignore_errors=True)
+    return {"bytes": nbytes, "save_s": round(t1 - t0, 3), "load_s": round(t2 - t1, 3),
+            "save_gb_s": round(nbytes / (t1 - t0) / 1e9, 2), "load_gb_s": round(nbytes / (t2 - t1) / 1e9, 2),
+            "reloaded_search_identical": same, "where": "a temporary file (the box's /tmp)"}
+
+
+def search_leg(rows: int, queries: int, k: int, device, world: int = 1, rank: int = 0, keep_host: bool = False,
+               persist_shard: bool = False):
     """BASELINE configs[4]: 10k fp16 query embeddings vs a rows x 512 fp16 index in HBM, top-k
     by exact cosine (fp16 MFMA pass + exact re-score of the candidates).
     world > 1: the index is row-sharded (rank r holds shard_range(rows, r, world)
@@ -345,6 +375,9 @@ def search_leg(rows: int, queries: int, k: int, device, world: int = 1, rank: in
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
         dt = float(t.item())
     st = idx.stats()
+    persist = None
+    if persist_shard and world == 1:
+        persist = shard_roundtrip(idx, q[:256], k)
     idx.close()
     # the check subset: gather every rank's exact top-k, order the union, compare with the fast path
     if world > 1:
@@ -363,6 +396,8 @@ def search_leg(rows: int, queries: int, k: int, device, world: int = 1, rank: in
                                "per-rank top-k gathered and ordered (score desc, index asc): indices and scores equal"},
            "rows_seeded": "by global row (2^20-row chunks, seed 7 + chunk): the same index at every world size",
            "topk_sha256": hashlib.sha256(i.cpu().numpy().tobytes()).hexdigest()[:16]}
+    if persist is not None:
+        out["persist"] = persist
     if world > 1:
         out.update({"n_gpus": world, "shard_rows": stop - start,
                     "parallelism": "row-sharded index, replicated queries, all_gather(top-k) + GPU merge"})
@@ -773,7 +808,7 @@ def main():
     if not args.no_search:   # every rank takes part when the index is sharded (world > 1)
         keep = rank == 0 and world == 1 and not args.no_cpu_baseline
         sr, host16, qs_host, gpu_i = search_leg(args.search_rows, args.search_queries, 5, dev, world, rank,
-                                                keep_host=keep)
+                                                keep_host=keep, persist_shard=not args.no_persist)
         if rank == 0:
             result["search"] = sr
     if rank == 0 and world == 1 and not args.no_l14:

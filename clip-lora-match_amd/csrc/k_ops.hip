@@ -547,17 +547,12 @@ __global__ __launch_bounds__(256) void text_plan_kernel(int B, int L, const int*
     counts[1] = nt;
   }
   for (int b = tid; b <= B; b += 256) offs[b] = s_off[b];
-  // packed row r -> b * L + (r - offs[b]): consecutive threads write consecutive rows (coalesced
-  // stores), each thread's caption cursor only moves forward (rows grow by 256 per step)
-  const int total = s_off[B];
-  int lo = 0, hi = B - 1;   // first row of this thread: largest b with s_off[b] <= tid
-  while (lo < hi) {
-    const int mid = (lo + hi + 1) >> 1;
-    if (s_off[mid] <= tid) lo = mid; else hi = mid - 1;
-  }
-  for (int r = tid, b = lo; r < total; r += 256) {
-    while (s_off[b + 1] <= r) ++b;
-    rowmap[r] = b * L + (r - s_off[b]);
+  // packed row r -> b * L + (r - offs[b]): caption by caption, all threads on one caption's rows
+  // (one coalesced store each; no dependent LDS chains: a per-thread caption cursor, and before it
+  // a per-caption serial loop, made this kernel 41 / 23 us)
+  for (int b = 0; b < B; ++b) {
+    const int o = s_off[b], n = s_off[b + 1] - o;
+    for (int p = tid; p < n; p += 256) rowmap[o + p] = b * L + p;
   }
 }
 
