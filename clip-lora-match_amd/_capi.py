@@ -103,9 +103,6 @@ def lib():
         "clm_attention": (c_int, [c_int, c_int, c_int, c_void_p, c_void_p, c_int64, c_int, c_int, c_int, c_void_p]),
         "clm_layernorm": (c_int, [c_int, c_int, c_void_p, c_int64, c_int64, c_int, c_void_p, c_void_p, c_float, c_void_p,
                                   c_int64, c_void_p]),
-        "clm_gemm_resid_ln": (c_int, [c_int, c_int, c_void_p, c_int64, c_void_p, c_int64, c_int, c_int, c_int, c_void_p,
-                                      c_int64, c_void_p, c_void_p, c_void_p, c_float, c_void_p, c_int64, c_int,
-                                      c_void_p]),
         "clm_prof_read": (c_int, [c_void_p, c_int, POINTER(ctypes.c_double), POINTER(ctypes.c_double),
                                   POINTER(c_int64)]),
     }
@@ -125,7 +122,7 @@ EXPORTED = (
     "clm_cosine_scores", "clm_topk_merge", "clm_l2_normalize", "clm_fuse_queries", "clm_resize_crop", "clm_synth_images", "clm_index_has_f32", "clm_index_export", "clm_index_import",
     "clm_last_error", "clm_version",
     "clm_model_desc_size", "clm_prof_enable", "clm_prof_read", "clm_gemm", "clm_gemm_num_configs",
-    "clm_attention", "clm_layernorm", "clm_debug_set", "clm_gemm_resid_ln",
+    "clm_attention", "clm_layernorm", "clm_debug_set",
 )
 CLM_EPI_STORE, CLM_EPI_GELU, CLM_EPI_RESID, CLM_EPI_SCORE = 0, 1, 2, 4
 CLM_PROF_GEMM, CLM_PROF_ATTN, CLM_PROF_LN, CLM_PROF_OTHER = 0, 1, 2, 3

@@ -508,16 +508,6 @@ LnArgs ln_into_x(clm_ctx* c, Tower& T, int64_t M, const float* g, const float* b
   return a;
 }
 
-// the fused residual GEMM + LayerNorm of a RESID GEMM g (out = h, the residual stream) into T.X
-ResLnArgs resid_ln_args(clm_ctx* c, Tower& T, const GemmArgs& g, const float* gamma, const float* beta,
-                        const int* mdev) {
-  ResLnArgs a{};
-  a.A = g.A; a.lda = g.lda; a.W = g.W; a.ldw = g.ldw; a.M = g.M; a.N = g.N; a.K = g.K;
-  a.h = (float*)g.out; a.ldh = g.ldo; a.bias = g.bias;
-  a.gamma = gamma; a.beta = beta; a.eps = c->desc.ln_eps; a.y = T.X; a.ldy = T.ldx; a.m_dev = mdev;
-  return a;
-}
-
 // Last-layer pruning (default; $CLM_NO_PRUNE=1 runs every row): the encoders return only the
 // pooled row of each item (vision CLS row 0, text first-EOS row: TF/models/clip/
 // modeling_clip.py:558-580, 650), and after the last layer's attention every op is row-wise
@@ -546,21 +536,6 @@ bool text_varlen_enabled() {
     v = (e && !atoi(e)) ? 0 : 1;
   }
   return v == 1 && !(g_gemm_debug & 32);
-}
-
-// Residual GEMM + next LayerNorm in one launch (k_resln.hip, whole-row tiles) where it is faster
-// than the RESID GEMM + ln4 pair: the text tower's out_proj -> LN2 (d = K = 512: 31.3 vs 24.8 +
-// 10.8 us at batch 256). Vision out_proj (45.0 vs 30.1 + 11.3), and fc2 -> LN1 of both towers
-// (106 vs 67.3 + 11.3, 64.1 vs 49.6 + 11.0) stay two launches: a whole-row tile streams all of W
-// through every CU (profiles/r03_v9_resln_probe.jsonl). $CLM_RESLN=0 turns it off (A/B runs);
-// merged / no LoRA only (unmerged mode's LayerNorm also emits the LoRA down-projection).
-bool resln_enabled(int d, int K) {
-  static int v = -1;
-  if (v < 0) {
-    const char* e = getenv("CLM_RESLN");
-    v = (e && !atoi(e)) ? 0 : 1;
-  }
-  return v == 1 && d == 512 && K == d && resid_ln_supported(d, K);
 }
 
 // q/k/v projection + attention fused into one launch for T <= 128 (k_gemm_attn.hip) unless
@@ -646,18 +621,14 @@ int run_layers(clm_ctx* c, Tower& T, int B, int S, bool causal, const int32_t* i
     g = GemmArgs{};
     g.A = O; g.lda = T.ldo; g.W = Lw.w_out; g.ldw = Lw.k_out; g.M = (int)M; g.N = T.d; g.K = Lw.k_out;
     g.out = h; g.ldo = T.d; g.bias = Lw.b_out;
-    const bool resln = resln_enabled(T.d, g.K) && !Lw.r_fc1;
-    if (resln) {   // the pooled rows too: bit-identical to their every-row run (no split-K)
-      ResLnArgs ra = resid_ln_args(c, T, g, Lw.ln2_g, Lw.ln2_b, pooled ? nullptr : mdev);
-      PROF(CLM_PROF_GEMM, 2.0 * (pooled ? (double)M : Mx) * g.N * g.K); KCHK(resid_ln(bf, ra, st));
-    } else if (pooled) {
+    if (pooled) {
       int r = pooled_resid(g);
       if (r) return r;
     } else {
       g.m_dev = mdev;
       PROF(CLM_PROF_GEMM, 2.0 * Mx * g.N * g.K); KCHK(gemm(bf, EPI_RESID, g, st));
     }
-    if (!resln) {
+    {
       LnArgs ln = ln_into_x(c, T, M, Lw.ln2_g, Lw.ln2_b, Lw.a_fc1, Lw.r_fc1, h);
       if (!pooled) ln.m_dev = mdev;
       PROF(CLM_PROF_LN, (pooled ? (double)M : Mx) * T.d * 6.0);
@@ -677,11 +648,6 @@ int run_layers(clm_ctx* c, Tower& T, int B, int S, bool causal, const int32_t* i
     if (pooled) {
       int r = pooled_resid(g);
       if (r) return r;
-    } else if (!last && resln_enabled(T.d, g.K) && !T.layers[l + 1].r_qkv) {
-      LayerW& Ln = T.layers[l + 1];
-      ResLnArgs ra = resid_ln_args(c, T, g, Ln.ln1_g, Ln.ln1_b, mdev);
-      PROF(CLM_PROF_GEMM, 2.0 * Mx * g.N * g.K); KCHK(resid_ln(bf, ra, st));
-      continue;
     } else {
       g.m_dev = mdev;
       PROF(CLM_PROF_GEMM, 2.0 * Mx * g.N * g.K); KCHK(gemm(bf, EPI_RESID, g, st));
@@ -829,27 +795,6 @@ int clm_layernorm(int hip_device, int dtype, const float* src, int64_t lds, int6
   a.g1 = gamma; a.b1 = beta; a.y = (u16*)y; a.ldy = ldy; a.M = (int)M; a.d = d; a.eps = eps;
   hipError_t e = layernorm(dtype == CLM_BF16, a, (hipStream_t)stream);
   if (e != hipSuccess) return fail(CLM_E_HIP, std::string("layernorm: ") + hipGetErrorString(e));
-  return CLM_OK;
-}
-
-int clm_gemm_resid_ln(int hip_device, int dtype, const void* A, int64_t lda, const void* W, int64_t ldw, int M, int N,
-                      int K, float* h, int64_t ldh, const float* bias, const float* gamma, const float* beta, float eps,
-                      void* y, int64_t ldy, int bm, void* stream) {
-  if (dtype != CLM_BF16 && dtype != CLM_F16) return fail(CLM_E_ARG, "dtype must be bf16 or f16");
-  if (!resid_ln_supported(N, K)) return fail(CLM_E_ARG, "resid_ln: N must be 512 or 768, K % 32 == 0");
-  if (M < 0 || K <= 0 || K % 32 || lda < K || ldw < K || ldh < N || ldy < N || (lda % 8) || (ldw % 8) || (ldh % 4) ||
-      (ldy % 8))
-    return fail(CLM_E_ARG, "bad shape");
-  if (bm != 0 && bm != 32 && bm != 64 && bm != 80) return fail(CLM_E_ARG, "bm must be 0, 32, 64 or 80");
-  if (!A || !W || !h || !gamma || !beta || !y) return fail(CLM_E_ARG, "null pointer");
-  if (M == 0) return CLM_OK;
-  DeviceGuard g(hip_device);
-  ResLnArgs a{};
-  a.A = (const u16*)A; a.lda = lda; a.W = (const u16*)W; a.ldw = ldw; a.M = M; a.N = N; a.K = K;
-  a.h = h; a.ldh = ldh; a.bias = bias; a.gamma = gamma; a.beta = beta; a.eps = eps; a.y = (u16*)y; a.ldy = ldy;
-  a.bm = bm; a.debug = g_gemm_debug & 3;
-  hipError_t e = resid_ln(dtype == CLM_BF16, a, (hipStream_t)stream);
-  if (e != hipSuccess) return fail(CLM_E_HIP, std::string("resid_ln: ") + hipGetErrorString(e));
   return CLM_OK;
 }
 

@@ -282,9 +282,8 @@ static_assert(GEMM_CFG_SPLITK == 2, "config 2 is the 128 x 64 tile");
 //    trip with the other's MFMAs.
 // $CLM_GEMM_CFG forces a config (tools and tests).
 struct CfgModel { int id, bm, bn, wg_per_cu; double eff; };
-// (9 / 11: the loader-wave G2S tiles, ~5 % over the 8-wave G2 256 x 128 / 128 x 256 they replaced)
 constexpr CfgModel MODELS_G2[] = {
-  {8, 256, 192, 1, 2.569}, {9, 256, 128, 1, 2.466}, {10, 192, 256, 1, 2.521}, {11, 128, 256, 1, 2.41}};
+  {8, 256, 192, 1, 2.569}, {9, 256, 128, 1, 2.349}, {10, 192, 256, 1, 2.521}, {11, 128, 256, 1, 2.340}};
 // 160x128 (config 7): the N = 512 / 768 RESID / PATCH shapes fill one round of 2-WG/CU slots
 // (480 / 496 tiles of 512, against 402 / 412 with 192x128): v_out 28.7 vs 32.0 µs, v_fc2 67.7
 // vs 74.9, t_out 24.0 vs 25.8, t_fc2 49.5 vs 53.7 (profiles/r02_v4_gemm_160x128.txt) -- when the

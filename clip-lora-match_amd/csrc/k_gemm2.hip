@@ -1,5 +1,5 @@
-// G2 MFMA GEMM for gfx950 (configs 8-11 of clm_gemm; 9 and 11 with loader waves, G2S): large
-// per-wave tiles, for the encoder's dense qkv / out / fc1 / fc2 GEMMs (TF/models/clip/modeling_clip.py:
+// G2 MFMA GEMM for gfx950 (configs 8-11 of clm_gemm): one wave per SIMD with large per-wave
+// tiles, for the encoder's dense qkv / out / fc1 / fc2 GEMMs (TF/models/clip/modeling_clip.py:
 // 294-297, 332, 343-344). Same operand layout, epilogues and persistent tile order as
 // k_gemm.hip's gemm_kernel; the main loop differs (see below).
 #include "gemm_common.hpp"
@@ -19,33 +19,24 @@ using namespace gemm_detail;
 // The LDS latency of every fragment read is covered by 64 MFMAs of the other half, the only
 // MFMA-idle window per step is the barrier, and DMA(s+2) is issued before a tile end's
 // epilogue stores, so the next wait never drains them (counted vmcnt).
-//
-// G2S (LW > 0 loader waves): the same ring and MFMA schedule, but the LDS-DMA is issued by LW
-// dedicated loader waves (one per SIMD beside one compute wave) that only wait, barrier and
-// issue; the WM x WN compute waves issue no vector-memory instruction in the main loop. Measured
-// on G2 (PMC, tools/gemm_lds_pmc.sh): 37-46 % of wave cycles stalled at instruction issue with
-// the MFMA pipe 32-34 % busy and the LDS 13 % busy -- an in-order wave's MFMAs wait behind its
-// own LDS-DMA pieces (each held at issue until the texture unit takes it); split roles let the
-// compute wave's MFMAs issue while its SIMD partner's DMA waits.
-template <int BM, int BN, int WM, int WN, int LW = 0>
+template <int BM, int BN, int WM, int WN>
 struct Cfg2 {
-  static constexpr int NW = WM * WN;           // compute waves
-  static constexpr int NL = LW > 0 ? LW : NW;  // waves that issue the DMA
-  static constexpr int NT = (NW + LW) * 64;
+  static constexpr int NW = WM * WN;
+  static constexpr int NT = NW * 64;
   static constexpr int TM = BM / WM / 16;
   static constexpr int TN = BN / WN / 16;
   static constexpr int STAGE_BYTES = (BM + BN) * BK * 2;
   static constexpr int LDS = 2 * STAGE_BYTES;   // two-buffer ring: DMA lead of one K-step
-  static constexpr int LA = BM / 8 / NL;
-  static constexpr int LB = BN / 8 / NL;
-  static_assert(BM % (8 * NL) == 0 && BN % (8 * NL) == 0, "rows must split evenly over the loading waves");
+  static constexpr int LA = BM / 8 / NW;
+  static constexpr int LB = BN / 8 / NW;
+  static_assert(BM % (8 * NW) == 0 && BN % (8 * NW) == 0, "rows must split evenly over waves");
 };
 
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
 
-template <bool BF, int EPI, int BM, int BN, int WM, int WN, int LW = 0>
-__global__ __launch_bounds__((WM * WN + LW) * 64, LW > 0 ? 2 : 1) void gemm2_kernel(GemmArgs ga) {
-  using C = Cfg2<BM, BN, WM, WN, LW>;
+template <bool BF, int EPI, int BM, int BN, int WM, int WN>
+__global__ __launch_bounds__(WM * WN * 64, 1) void gemm2_kernel(GemmArgs ga) {
+  using C = Cfg2<BM, BN, WM, WN>;
   GemmArgs g = ga;   // varlen: the device-resident row count (the grid was sized for ga.M)
   if (g.m_dev) g.M = __builtin_amdgcn_readfirstlane(*g.m_dev);
   constexpr int L = C::LA + C::LB;   // vmcnt units (DMA instructions) per K-step
@@ -54,8 +45,6 @@ __global__ __launch_bounds__((WM * WN + LW) * 64, LW > 0 ? 2 : 1) void gemm2_ker
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wid / WN, wn = wid % WN;
-  const bool loader = LW > 0 && wid >= C::NW;
-  const int lid = LW > 0 ? wid - C::NW : wid;   // index among the DMA-issuing waves
   const int ntn = (g.N + BN - 1) / BN, ntm = (g.M + BM - 1) / BM;
   const int ntiles = ntn * ntm, G = gridDim.x;
   const TileWalk tw = tile_walk(ntiles, G);
@@ -107,13 +96,13 @@ __global__ __launch_bounds__((WM * WN + LW) * 64, LW > 0 ? 2 : 1) void gemm2_ker
     const int so = __builtin_amdgcn_readfirstlane(ld_kt * BK * 2);
 #pragma unroll
     for (int j = 0; j < C::LA; ++j)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, (lds_ptr_t)(base + (lid * C::LA + j) * 1024), 16,
-                                               (la0 + (uint32_t)((lid * C::LA + j) & 1) * dch) + (uint32_t)((lid * C::LA + j) * 8) * lda2,
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, (lds_ptr_t)(base + (wid * C::LA + j) * 1024), 16,
+                                               (la0 + (uint32_t)((wid * C::LA + j) & 1) * dch) + (uint32_t)((wid * C::LA + j) * 8) * lda2,
                                                so, 0, 0);
 #pragma unroll
     for (int j = 0; j < C::LB; ++j)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rw, (lds_ptr_t)(base + BM * 128 + (lid * C::LB + j) * 1024), 16,
-                                               (lw0 + (uint32_t)((lid * C::LB + j) & 1) * dch) + (uint32_t)((lid * C::LB + j) * 8) * ldw2,
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rw, (lds_ptr_t)(base + BM * 128 + (wid * C::LB + j) * 1024), 16,
+                                               (lw0 + (uint32_t)((wid * C::LB + j) & 1) * dch) + (uint32_t)((wid * C::LB + j) * 8) * ldw2,
                                                so, 0, 0);
     if (++ld_kt == nk) {
       ld_kt = 0;
@@ -141,30 +130,10 @@ __global__ __launch_bounds__((WM * WN + LW) * 64, LW > 0 ? 2 : 1) void gemm2_ker
       for (int nb = 0; nb < TN; ++nb) acc[mb][nb] = mfma16<BF>(bw[nb], af[mb], acc[mb][nb]);
   };
 
-  if constexpr (LW > 0) {
-    if (loader) {   // the ring alone: the compute waves' barriers, one per K-step after the first
-      dma_next(0);
-      if (S > 1) dma_next(1);
-      if (S >= 2) wait_vmcnt<L>();
-      else wait_vmcnt<0>();
-      lds_barrier();
-      int cur = 0;
-      for (int s = 0; s < S; ++s) {
-        if (s + 1 < S) {
-          wait_vmcnt<0>();   // DMA(s+1) landed (a loader wave has no other memory operations)
-          lds_barrier();
-          if (s + 2 < S) dma_next(cur);
-        }
-        cur ^= 1;
-      }
-      return;
-    }
-  } else {
-    dma_next(0);
-    if (S > 1) dma_next(1);
-    if (S >= 2) wait_vmcnt<L>();   // DMA(0) retired, DMA(1) in flight
-    else wait_vmcnt<0>();
-  }
+  dma_next(0);
+  if (S > 1) dma_next(1);
+  if (S >= 2) wait_vmcnt<L>();   // DMA(0) retired, DMA(1) in flight
+  else wait_vmcnt<0>();
   lds_barrier();
   u32x4 a0[TM], b0[TN], a1[TM], b1[TN];
   read_frags(smem, 0, a0, b0);
@@ -189,12 +158,10 @@ __global__ __launch_bounds__((WM * WN + LW) * 64, LW > 0 ? 2 : 1) void gemm2_ker
         // DMA(s+1) retired -- kk1 fragments of s landed, and after the barrier no wave reads
         // buffer `cur` any more. The previous tile's E epilogue stores were issued after DMA(s+1)
         // of its last step, so at kt = 0 they may stay in flight.
-        if constexpr (LW == 0) {
-          if (kt == 0 && ti > 0 && vec_epi) wait_vmcnt<E>();
-          else wait_vmcnt<0>();
-        }
+        if (kt == 0 && ti > 0 && vec_epi) wait_vmcnt<E>();
+        else wait_vmcnt<0>();
         lds_barrier();
-        if (LW == 0 && s + 2 < S) dma_next(cur);
+        if (s + 2 < S) dma_next(cur);
         read_frags(smem + nxt * C::STAGE_BYTES, 0, a0, b0);
       }
       mma(a1, b1);
@@ -211,10 +178,10 @@ __global__ __launch_bounds__((WM * WN + LW) * 64, LW > 0 ? 2 : 1) void gemm2_ker
   }
 }
 
-template <bool BF, int EPI, int BM, int BN, int WM, int WN, int LW = 0>
+template <bool BF, int EPI, int BM, int BN, int WM, int WN>
 hipError_t launch_cfg2(const GemmArgs& g, hipStream_t s) {
-  using C = Cfg2<BM, BN, WM, WN, LW>;
-  auto kern = gemm2_kernel<BF, EPI, BM, BN, WM, WN, LW>;
+  using C = Cfg2<BM, BN, WM, WN>;
+  auto kern = gemm2_kernel<BF, EPI, BM, BN, WM, WN>;
   static unsigned dev_done = 0;
   int dev = 0;
   (void)hipGetDevice(&dev);
@@ -240,11 +207,9 @@ template <bool BF, int EPI>
 hipError_t by_id(int id, const GemmArgs& g, hipStream_t s) {
   switch (id) {
     case 8: return launch_cfg2<BF, EPI, 256, 192, 4, 2>(g, s);
-    // G2S, 4 compute + 4 loader waves: vision / text fc1 71.6 / 50.9 us against 74.7 / 54.1 for the
-    // 8-wave G2 256 x 128 they replace (profiles/r03_v9_g2s_probe.jsonl)
-    case 9: return launch_cfg2<BF, EPI, 256, 128, 2, 2, 4>(g, s);
+    case 9: return launch_cfg2<BF, EPI, 256, 128, 4, 2>(g, s);
     case 10: return launch_cfg2<BF, EPI, 192, 256, 2, 4>(g, s);
-    case 11: return launch_cfg2<BF, EPI, 128, 256, 2, 2, 4>(g, s);
+    case 11: return launch_cfg2<BF, EPI, 128, 256, 2, 4>(g, s);
     default: return hipErrorInvalidValue;
   }
 }

@@ -58,25 +58,6 @@ int gemm_num_configs();
 // other stream; alone, the slot-filling 160x128 tiles are faster (profiles/r02_v4_gemm_160x128.txt)
 void gemm_set_concurrent(bool on);
 
-// Residual GEMM + the next LayerNorm in one launch (k_resln.hip), N = d in {512, 768}:
-//   h[m, :] += A[m, :] . W^T + bias;  y[m, :] = LayerNorm(h[m, :]; gamma, beta) (compute dtype)
-// Whole-row tiles (bm rows per workgroup, 0 = resid_ln_bm(M)); K % 32 == 0.
-struct ResLnArgs {
-  const u16* A; int64_t lda;
-  const u16* W; int64_t ldw;
-  int M, N, K;
-  float* h; int64_t ldh;
-  const float* bias;
-  const float* gamma; const float* beta; float eps;
-  u16* y; int64_t ldy;
-  const int* m_dev;   // varlen: device-resident row count (<= M, which sizes the grid)
-  int bm;
-  int debug;          // diagnostics only: 1 = main loop only, 2 = no LayerNorm (residual update only)
-};
-hipError_t resid_ln(bool bf16, const ResLnArgs& a, hipStream_t s);
-bool resid_ln_supported(int d, int K);   // d in {512, 768}, K % 32 == 0
-int resid_ln_bm(int M);
-
 // ----------------------------------------------------------- row ops -------
 // LayerNorm over rows of a fp32 matrix, one wave per row.
 //   mode 0: x = src rows                         (src = h)

@@ -228,14 +228,6 @@ int clm_attention(int hip_device, int dtype, int causal, const void* qkv, void* 
 int clm_layernorm(int hip_device, int dtype, const float* src, int64_t lds, int64_t M, int d,
                   const float* gamma, const float* beta, float eps, void* y, int64_t ldy, void* stream);
 
-/* Residual GEMM with the next LayerNorm fused (the encoder's out_proj -> LN2 and fc2 -> next LN1,
- * TF/models/clip/modeling_clip.py:362-384): h[m, :] += A[m, :] . W^T + bias (fp32 h [M, ldh]), then
- * y[m, :] = LayerNorm(h[m, :]; gamma, beta, eps) in dtype (y [M, ldy]); N = d in {512, 768},
- * K % 32 == 0, bm = rows per workgroup (0 = heuristic, 32, 64 or 80); device pointers */
-int clm_gemm_resid_ln(int hip_device, int dtype, const void* A, int64_t lda, const void* W, int64_t ldw, int M, int N,
-                      int K, float* h, int64_t ldh, const float* bias, const float* gamma, const float* beta, float eps,
-                      void* y, int64_t ldy, int bm, void* stream);
-
 /* Kernel timing by category, measured with hipEvents recorded on the launch
  * stream around every kernel of clm_encode_* while enabled (adds event
  * overhead; keep it off in timed regions). categories: CLM_PROF_* */

@@ -272,72 +272,6 @@ def test_layernorm_vs_torch_and_row_invariant(dtype, d):
         assert torch.equal(_ln(dtype, x[rows].contiguous(), gam, bet), y[rows]), rows
 
 
-def _resid_ln(dtype, A, W, h, bias, gam, bet, y, bm=0, eps=1e-5):
-    M, K = A.shape
-    C.check(C.lib().clm_gemm_resid_ln(0, DT[dtype][1], C.ptr(A), A.stride(0), C.ptr(W), W.stride(0), M, W.shape[0], K,
-                                      C.ptr(h), h.stride(0), C.ptr(bias) if bias is not None else None, C.ptr(gam),
-                                      C.ptr(bet), eps, C.ptr(y), y.stride(0), bm, C.stream_of(A.device)),
-            "clm_gemm_resid_ln")
-
-
-@pytest.mark.parametrize("dtype", ["bfloat16", "float16"])
-@pytest.mark.parametrize("N,K", [(768, 768), (768, 3072), (512, 512), (512, 2048)])
-@pytest.mark.parametrize("M", [333, 2000])
-def test_resid_ln_vs_torch_and_resid_gemm(dtype, N, K, M):
-    """The fused residual GEMM + LayerNorm (out_proj -> LN2, fc2 -> next LN1): h is bit-identical to
-    the RESID GEMM's (same K order, same h + (acc + bias)); y is torch's fp32 LayerNorm of that h to
-    one 16-bit rounding; every row tiling (32 / 64 / 80 rows per workgroup) give the same bits, and
-    nothing outside [M, N) of h or y is written."""
-    td = DT[dtype][0]
-    g = torch.Generator(device="cuda").manual_seed(M + N + K)
-    A = torch.randn((M, K), generator=g, device="cuda").to(td)
-    W = (torch.randn((N, K), generator=g, device="cuda") / K ** 0.5).to(td)
-    bias = torch.randn(N, generator=g, device="cuda")
-    gam = torch.randn(N, generator=g, device="cuda")
-    bet = torch.randn(N, generator=g, device="cuda")
-    h0 = torch.randn((M + 40, N + 12), generator=g, device="cuda") * 3 + torch.randn((M + 40, 1), generator=g,
-                                                                                   device="cuda") * 5
-    want_h = h0[:M, :N].clone()
-    _gemm(dtype, C.CLM_EPI_RESID, -1, A, W, want_h, bias)
-    y0 = torch.full((M + 40, N + 24), 3.0, device="cuda").to(td)
-    ref_y = torch.nn.functional.layer_norm(want_h, (N,), gam, bet, 1e-5)
-    ulp = 2.0 ** (-8 if dtype == "bfloat16" else -11)
-    first = None
-    for bm in (0, 32, 64, 80):
-        h = h0.clone()
-        y = y0.clone()
-        _resid_ln(dtype, A, W, h[:M, :N], bias, gam, bet, y[:M, :N], bm)
-        assert torch.equal(h[:M, :N], want_h), bm
-        assert torch.equal(h[:, N:], h0[:, N:]) and torch.equal(h[M:], h0[M:]), bm
-        assert torch.equal(y[:, N:], y0[:, N:]) and torch.equal(y[M:], y0[M:]), bm
-        err = (y[:M, :N].float() - ref_y).abs() - (ulp * ref_y.abs() + 1e-5)
-        assert (err <= 0).all(), (bm, float(err.max()))
-        if first is None:
-            first = y[:M, :N].clone()
-        assert torch.equal(y[:M, :N], first), bm
-
-
-def test_resid_ln_rows_independent_of_batch():
-    """A row's h and y bits do not depend on the row count or on the row's place in its tile."""
-    dtype, N, K, Mfull = "float16", 768, 768, 250
-    g = torch.Generator(device="cuda").manual_seed(11)
-    A = torch.randn((Mfull, K), generator=g, device="cuda").half()
-    W = (torch.randn((N, K), generator=g, device="cuda") / K ** 0.5).half()
-    bias, gam, bet = (torch.randn(N, generator=g, device="cuda") for _ in range(3))
-    h0 = torch.randn((Mfull, N), generator=g, device="cuda")
-
-    def run(rows):
-        h = h0[rows].clone()
-        y = torch.empty((len(rows), N), dtype=torch.half, device="cuda")
-        _resid_ln(dtype, A[rows].contiguous(), W, h, bias, gam, bet, y)
-        return h, y
-
-    rh, ry = run(list(range(Mfull)))
-    for rows in (list(range(200, 250)), [249, 3, 77, 200, 5], [249], list(range(50, 250))):
-        h, y = run(rows)
-        assert torch.equal(h, rh[rows]) and torch.equal(y, ry[rows]), len(rows)
-
-
 def test_c_abi_under_host_sanitizers_with_device():
     """The prebuilt host-sanitizer harness (csrc/Makefile `sanitize`, ASan + UBSan on the host
     half) over the index lifecycle and the host-buffer entry points, results checked against
