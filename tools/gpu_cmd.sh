@@ -1,6 +1,4 @@
 #!/bin/bash
 # scratch GPU session script (the command of the last gpurun call)
 cd "$(dirname "$0")/.." && export TMPDIR=/tmp && mkdir -p gpurun_out
-timeout -k 10 700 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1; rc=$?; tail -3 gpurun_out/pytest_gpu.log; [ $rc -eq 0 ] || exit $rc
-timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1; rc=$?; tail -2 gpurun_out/smoke.log; [ $rc -eq 0 ] || exit $rc
-timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python3 bench.py --no-search --no-cpu-baseline --no-l14 --no-varlen --no-index-build --no-unmerged > gpurun_out/prof.log 2>&1; rc=$?; echo prof rc=$rc; [ $rc -eq 0 ] || exit $rc
+ARMS="A=A B=B" bash tools/ab_lib.sh
