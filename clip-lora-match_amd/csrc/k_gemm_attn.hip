@@ -117,6 +117,14 @@ __global__ __launch_bounds__(FA_NW * 64, 2) void gemm_attn_kernel(FaArgs a) {
   };
 
   const int wm = wid / FA_WN, wn = wid % FA_WN;
+  // the epilogue's bias vectors, loaded before the main loop (their latency hides under it instead
+  // of opening the q/k/v staging)
+  float4 bv[FA_TN];
+#pragma unroll
+  for (int nb = 0; nb < FA_TN; ++nb) {
+    const int col = wn * (FA_BN / FA_WN) + nb * 16 + 4 * g;
+    bv[nb] = a.bias ? *(const float4*)(a.bias + (col >> 6) * a.d + h * 64 + (col & 63)) : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
   f32x4 acc[FA_TM][FA_TN];
 #pragma unroll
   for (int i = 0; i < FA_TM; ++i)
@@ -154,12 +162,6 @@ __global__ __launch_bounds__(FA_NW * 64, 2) void gemm_attn_kernel(FaArgs a) {
   // ---- q / k / v -> compute dtype, staged in LDS (sections [256 rows][128 B], swizzled) -----
   // lane holds row wm*64 + mb*16 + (lane & 15), columns wn*96 + nb*16 + 4g .. +3 of the tile:
   // section (q, k, v) = column / 64, head dim = column % 64
-  float4 bv[FA_TN];
-#pragma unroll
-  for (int nb = 0; nb < FA_TN; ++nb) {
-    const int col = wn * (FA_BN / FA_WN) + nb * 16 + 4 * g;
-    bv[nb] = a.bias ? *(const float4*)(a.bias + (col >> 6) * a.d + h * 64 + (col & 63)) : make_float4(0.f, 0.f, 0.f, 0.f);
-  }
   lds_barrier();   // every wave has read its last fragments out of the ring
 #pragma unroll
   for (int mb = 0; mb < FA_TM; ++mb) {
