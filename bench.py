@@ -52,6 +52,10 @@ from clip_lora_match_amd import weights as W  # noqa: E402
 from clip_lora_match_amd.engine import ClipLoraModel  # noqa: E402
 
 MFMA_PEAK_TFLOPS = 2500.0   # dense bf16/fp16 MFMA, MI355X (MI355X_MICROARCH.md chip table)
+# what the chip sustains on a pure back-to-back v_mfma_f32_16x16x32_f16 stream with random operands
+# (tools/mfma_probe.hip, 256-1024 workgroups of 8 waves: 1.98-2.03 PF/s; the clock drops under
+# MFMA load), profiles/r03_v10_mfma_peak_probe.jsonl; reported beside the list peak, not used for frac
+MFMA_SUSTAINED_TFLOPS = 2028.0
 HBM_PEAK_GBS = 8000.0
 METRIC = "image+text embeds/sec & cosine top-k QPS, ViT-B/32+LoRA, 1/2/4/8 MI355X"
 
@@ -752,6 +756,10 @@ def main():
             "bound": "mfma",
             "achieved": round(gemm_flops / (gemm_ms * 1e-3) / 1e12, 2),
             "peak": MFMA_PEAK_TFLOPS,
+            "sustained_mfma_peak": {"value": MFMA_SUSTAINED_TFLOPS,
+                                    "frac": round(gemm_flops / (gemm_ms * 1e-3) / 1e12 / MFMA_SUSTAINED_TFLOPS, 4),
+                                    "source": "tools/mfma_probe.hip: MFMA-only loop, random fp16 operands "
+                                              "(profiles/r03_v10_mfma_peak_probe.jsonl)"},
             "unit": "TFLOP/s",
             "frac": round(gemm_flops / (gemm_ms * 1e-3) / 1e12 / MFMA_PEAK_TFLOPS, 4),
             "traffic": pmc.get("gemm_mean_hbm_bytes_per_launch"),
