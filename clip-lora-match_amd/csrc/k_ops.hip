@@ -498,8 +498,8 @@ __global__ __launch_bounds__(256) void text_lens_kernel(const int32_t* ids, int 
 // in the prefix sums), then thread 0 chains the tiles from caption 0 (one LDS read per tile).
 // (A sequential per-caption pass in one wave cost 40-110 us at B = 256.)
 constexpr int PLAN_MAX_B = 4096;
-__global__ __launch_bounds__(256) void text_plan_kernel(int B, int L, const int* lens, int* offs, int* rowmap,
-                                                        int* tiles, int* counts) {
+__global__ __launch_bounds__(256) void text_plan_kernel(int B, int L, const int* lens, int* offs, int* tiles,
+                                                        int* counts) {
   __shared__ int s_off[PLAN_MAX_B + 1];
   __shared__ int s_next[PLAN_MAX_B];
   __shared__ int s_part[256];
@@ -547,12 +547,27 @@ __global__ __launch_bounds__(256) void text_plan_kernel(int B, int L, const int*
     counts[1] = nt;
   }
   for (int b = tid; b <= B; b += 256) offs[b] = s_off[b];
-  // packed row r -> b * L + (r - offs[b]): caption by caption, all threads on one caption's rows
-  // (one coalesced store each; no dependent LDS chains: a per-thread caption cursor, and before it
-  // a per-caption serial loop, made this kernel 41 / 23 us)
-  for (int b = 0; b < B; ++b) {
-    const int o = s_off[b], n = s_off[b + 1] - o;
-    for (int p = tid; p < n; p += 256) rowmap[o + p] = b * L + p;
+}
+
+// packed row r -> b * L + (r - offs[b]) (text_plan's row map), in parallel: workgroup w owns
+// captions [16 w, 16 w + 16) and their rows (contiguous in the packed order); each thread finds its
+// rows' caption by a 4-step binary search over the 17 offsets in LDS, and stores coalesced. (Filled
+// inside the one-workgroup plan kernel, caption by caption, this took ~50 of its 61 us per call.)
+constexpr int ROWMAP_CAPS = 16;
+__global__ __launch_bounds__(256) void text_rowmap_kernel(int B, int L, const int* offs, int* rowmap) {
+  __shared__ int s_o[ROWMAP_CAPS + 1];
+  const int b0 = blockIdx.x * ROWMAP_CAPS, nb = min(ROWMAP_CAPS, B - b0);
+  if (threadIdx.x <= nb) s_o[threadIdx.x] = offs[b0 + threadIdx.x];
+  __syncthreads();
+  const int o0 = s_o[0], n = s_o[nb] - o0;
+  for (int p = threadIdx.x; p < n; p += 256) {
+    const int r = o0 + p;
+    int lo = 0, hi = nb - 1;   // the last j with s_o[j] <= r
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (s_o[mid] <= r) lo = mid; else hi = mid - 1;
+    }
+    rowmap[r] = (b0 + lo) * L + (r - s_o[lo]);
   }
 }
 
@@ -731,7 +746,8 @@ hipError_t text_plan(const int32_t* ids, int B, int L, int eos, int* lens, int* 
   if (L < 1 || L > 256) return hipErrorInvalidValue;
   if (B > PLAN_MAX_B) return hipErrorInvalidValue;
   text_lens_kernel<<<(B + 3) / 4, 256, 0, s>>>(ids, B, L, eos, lens);
-  text_plan_kernel<<<1, 256, 0, s>>>(B, L, lens, offs, rowmap, tiles, counts);
+  text_plan_kernel<<<1, 256, 0, s>>>(B, L, lens, offs, tiles, counts);
+  text_rowmap_kernel<<<(B + ROWMAP_CAPS - 1) / ROWMAP_CAPS, 256, 0, s>>>(B, L, offs, rowmap);
   return hipGetLastError();
 }
 

@@ -130,8 +130,8 @@ hipError_t pool_project(const float* h, int64_t ldh, int B, int T, int d, const 
 // cannot reach the pooled output). Per caption b of ids [B, L]: lens[b] = pooled row + 1 live
 // rows, offs[b] = their exclusive prefix sum (offs[B] = total), rowmap[offs[b] + p] = b * L + p,
 // the fused-attention tiles (whole captions, <= 256 rows each; tiles[t] = first caption |
-// captions << 16) and counts = {live rows, tiles}. Two launches (lengths: a wave per caption;
-// prefix / packing / row map: one workgroup); B <= 4096.
+// captions << 16) and counts = {live rows, tiles}. Three launches (lengths: a wave per caption;
+// prefix / tiles: one workgroup; row map: a workgroup per 16 captions); B <= 4096.
 hipError_t text_plan(const int32_t* ids, int B, int L, int eos, int* lens, int* offs, int* rowmap, int* tiles,
                      int* counts, hipStream_t s);
 
