@@ -1,7 +1,8 @@
 """Multi-rank GPU paths on one MI355X: world 2 over gloo (RCCL refuses two ranks
 per device; the driver's 8-GPU node runs the RCCL path). The product's own sharded index build
 and row-sharded search with the GPU merge must equal the single-rank results bit for bit, and
-bench.py --gpus 2 must start and report 2 ranks by itself."""
+bench.py --gpus 2 must start and report 2 ranks by itself. The RCCL entry points themselves run
+in test_rccl_collectives (one rank per GPU the box has)."""
 import json
 import os
 import socket
@@ -38,6 +39,25 @@ def test_sharded_build_and_search_world2(tmp_path):
         assert r[key], (key, r)
     assert r["planted_top1"] == [5, 150_000, 150_001, 299_999]
     assert r["big_file_rows"] == 65_536
+
+
+def test_rccl_collectives(tmp_path):
+    """Every collective of the product and bench.py through an RCCL ("nccl") process group on the
+    box's GPU(s): one rank per visible GPU (one on a 1-GPU box)."""
+    import torch
+    world = max(torch.cuda.device_count(), 1)
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
+           "--master-addr=127.0.0.1", f"--master-port={_port()}", os.path.join(REPO, "tests", "rccl_worker.py"),
+           str(tmp_path)]
+    p = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=180)
+    assert p.returncode == 0, p.stderr[-3000:]
+    for r in range(world):
+        res = json.loads((tmp_path / f"rank{r}.json").read_text())
+        assert res["world"] == world and "nccl" in res["backend"], res
+        for key in ("all_gather_rows_equal", "gather_candidates_equal", "merge_sorted", "max_all_reduce",
+                    "broadcast_object", "host_all_reduce"):
+            assert res[key], (key, res)
 
 
 def test_bench_spawns_its_own_ranks(tmp_path):
