@@ -87,6 +87,7 @@ def parse_args(argv=None):
     ap.add_argument("--index-images", type=int, default=1_000_000, help="images of the configs[2] index build")
     ap.add_argument("--index-batch", type=int, default=512)
     ap.add_argument("--no-persist", action="store_true", help="skip the search index shard save / load timing")
+    ap.add_argument("--no-near-dup", action="store_true", help="skip the near-duplicate-rows search leg")
     ap.add_argument("--sequential", action="store_true", help="towers back to back on one stream, no graph")
     ap.add_argument("--split", type=int, default=0, help="sub-batches per tower in encode_pair (0 = library default)")
     return ap.parse_args(argv)
@@ -406,6 +407,52 @@ def search_leg(rows: int, queries: int, k: int, device, world: int = 1, rank: in
         out.update({"n_gpus": world, "shard_rows": stop - start,
                     "parallelism": "row-sharded index, replicated queries, all_gather(top-k) + GPU merge"})
     return out, host16, q.cpu(), i.cpu()
+
+
+def near_dup_search_leg(device, rows: int = 1_000_000, groups: int = 64, group_rows: int = 8192,
+                        queries: int = 1024, k: int = 5):
+    """Search over near-duplicate rows (a finder index built from one description
+    template puts thousands of rows inside the candidate window): `groups` tie groups of
+    `group_rows` rows (center + 1e-3 noise) spread through `rows` Gaussian rows, queries at the
+    group centers plus random ones. Every query near a center overflows its candidate list
+    (> 2048 candidates), so the block's overflowed queries are re-scanned exactly, together.
+    Reports QPS, the path counts (overflow) and whether the result equals the full exact scan
+    of every query (CLM_SEARCH_FULL, untimed)."""
+    from clip_lora_match_amd.search import CosineIndex
+    dim = 512
+    g = torch.Generator(device=device).manual_seed(91)
+    x = torch.randn((rows, dim), generator=g, device=device)
+    centers = torch.randn((groups, dim), generator=g, device=device)
+    stride = rows // groups
+    for j in range(groups):
+        a = j * stride
+        x[a:a + group_rows] = centers[j] + 1e-3 * torch.randn((group_rows, dim), generator=g, device=device)
+    x = (x / x.norm(dim=-1, keepdim=True)).half()
+    idx = CosineIndex(dim, capacity=rows, device=device)
+    idx.append(x)
+    del x
+    nc = groups * max((queries - 64) // groups, 0)   # center queries; the last >= 64 are random
+    q = torch.cat([centers.repeat(max(nc // groups, 1), 1)[:nc],
+                   torch.randn((queries - nc, dim), generator=g, device=device)])
+    q = (q / q.norm(dim=-1, keepdim=True)).half()
+    idx.search(q, k)   # untimed: workspace sizing
+    torch.cuda.synchronize()
+    before = idx.stats()
+    t0 = time.perf_counter()
+    s, i = idx.search(q, k)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    after = idx.stats()
+    os.environ["CLM_SEARCH_FULL"] = "1"
+    try:
+        s_ref, i_ref = idx.search(q, k)
+    finally:
+        os.environ.pop("CLM_SEARCH_FULL", None)
+    idx.close()
+    return {"qps": round(queries / dt, 1), "seconds": round(dt, 4), "rows": rows, "queries": queries, "k": k,
+            "tie_groups": groups, "group_rows": group_rows,
+            "paths_timed_block": {key: after[key] - before.get(key, 0) for key in after},
+            "equal_to_full_exact_scan": bool(torch.equal(i, i_ref) and torch.equal(s, s_ref))}
 
 
 def l14_leg(device, batch: int = 128, steps: int = 3, warmup: int = 1, dtype: str = "float16"):
@@ -819,6 +866,11 @@ def main():
                                                 keep_host=keep, persist_shard=not args.no_persist)
         if rank == 0:
             result["search"] = sr
+    if rank == 0 and world == 1 and not args.no_search and not args.no_near_dup:
+        try:
+            result["search_near_dup"] = near_dup_search_leg(dev)
+        except Exception as e:  # report, never hide
+            result["search_near_dup"] = {"error": repr(e)}
     if rank == 0 and world == 1 and not args.no_l14:
         try:
             result["l14"] = l14_leg(dev, dtype=args.dtype)

@@ -1411,6 +1411,91 @@ static int search_scan(clm_index* x, bool exact, const u16* q16, const float* qi
   return CLM_OK;
 }
 
+// Overflowed queries, wide path: their fp16 rows, inverse norms, fp32 rows, norms and filter
+// thresholds are gathered, the EPI_FILTER GEMM streams the index once more for just them with a
+// capacity of cap[j] (the first pass's count plus headroom), and rescore_wide + topk_merge pick the
+// exact top k from the whole list; results are scattered back to the queries' rows. Queries whose
+// list still exceeds its capacity are appended to `full` (the exact scan redoes them).
+static int overflow_wide(clm_index* x, const std::vector<int64_t>& qs, const std::vector<int64_t>& cap,
+                         const u16* q16, const float* qinv, const float* q32, const double* qn, const float* th,
+                         int k, float* osc, int64_t* oix, std::vector<int64_t>& full, hipStream_t st) {
+  const int dim = (int)x->dim;
+  const int64_t n = (int64_t)qs.size();
+  const void* xrows = x->rows32 ? (const void*)x->rows32 : (const void*)x->rows;
+  int64_t cap_max = 0;
+  for (int64_t c : cap) cap_max = std::max(cap_max, c);
+  cap_max = round_up(cap_max, RESCORE_WIDE_CHUNK);
+  const int64_t nch = cap_max / RESCORE_WIDE_CHUNK;
+  // queries per group: candidate lists (12 B per slot) within ~1 GB, at most 4096
+  const int64_t G = std::max<int64_t>(1, std::min<int64_t>(std::min<int64_t>(n, 4096), (int64_t)(1 << 30) / (cap_max * 12)));
+  size_t off = 0;
+  auto take = [&](size_t bytes) { size_t o = off; off = round_up(off + bytes, 256); return o; };
+  const size_t p_x = take((size_t)G * 8), p_q16 = take((size_t)G * dim * 2), p_qi = take((size_t)G * 4),
+               p_q32 = take((size_t)G * dim * 4), p_qn = take((size_t)G * 8), p_th = take((size_t)G * 4),
+               p_cnt = take((size_t)G * 4), p_cs = take((size_t)G * cap_max * 4), p_ci = take((size_t)G * cap_max * 8),
+               p_ps = take((size_t)G * nch * k * 4), p_pi = take((size_t)G * nch * k * 8),
+               p_s = take((size_t)G * k * 4), p_i = take((size_t)G * k * 8);
+  uint8_t* w = nullptr;
+  if (hipMalloc(&w, off) != hipSuccess) { (void)hipGetLastError(); return fail(CLM_E_OOM, "overflow workspace"); }
+  int64_t* gx = (int64_t*)(w + p_x);
+  int* cnt = (int*)(w + p_cnt);
+  std::vector<int> hcnt;
+  hipError_t e = hipSuccess;
+  int r = CLM_OK;
+  for (int64_t g0 = 0; g0 < n && e == hipSuccess && r == CLM_OK; g0 += G) {
+    const int64_t ng = std::min(G, n - g0);
+    e = hipMemcpyAsync(gx, qs.data() + g0, (size_t)ng * 8, hipMemcpyHostToDevice, st);
+    if (e == hipSuccess) e = gather_rows(q16, (int64_t)dim * 2, gx, ng, (int64_t)dim * 2, w + p_q16, (int64_t)dim * 2, false, st);
+    if (e == hipSuccess) e = gather_rows(qinv, 4, gx, ng, 4, w + p_qi, 4, false, st);
+    if (e == hipSuccess) e = gather_rows(q32, (int64_t)dim * 4, gx, ng, (int64_t)dim * 4, w + p_q32, (int64_t)dim * 4, false, st);
+    if (e == hipSuccess) e = gather_rows(qn, 8, gx, ng, 8, w + p_qn, 8, false, st);
+    if (e == hipSuccess) e = gather_rows(th, 4, gx, ng, 4, w + p_th, 4, false, st);
+    if (e == hipSuccess) e = hipMemsetAsync(cnt, 0, (size_t)ng * 4, st);
+    if (e != hipSuccess) break;
+    GemmArgs gf{};
+    gf.A = (const u16*)(w + p_q16); gf.lda = dim; gf.W = x->rows; gf.ldw = dim;
+    gf.M = (int)ng; gf.N = (int)x->n; gf.K = dim;
+    gf.rscale = (const float*)(w + p_qi); gf.cscale = x->inv;
+    gf.theta = (const float*)(w + p_th); gf.theta_ld = 1;
+    gf.cnt = cnt; gf.cand_s = (float*)(w + p_cs); gf.cand_i = (int64_t*)(w + p_ci); gf.cap = (int)cap_max;
+    gf.base = x->offset; gf.m_fastest = 1;
+    if ((e = gemm(false, EPI_FILTER, gf, st)) != hipSuccess) break;
+    if ((e = rescore_wide((const int64_t*)(w + p_ci), cnt, cap_max, (const float*)(w + p_q32),
+                          (const double*)(w + p_qn), dim, xrows, !x->rows32, x->offset, ng, k, (float*)(w + p_ps),
+                          (int64_t*)(w + p_pi), st)) != hipSuccess) break;
+    if ((e = topk_merge((const float*)(w + p_ps), (const int64_t*)(w + p_pi), ng, (int)nch, k, k, (float*)(w + p_s),
+                        (int64_t*)(w + p_i), st)) != hipSuccess) break;
+    hcnt.resize(ng);
+    if ((e = hipMemcpyAsync(hcnt.data(), cnt, (size_t)ng * 4, hipMemcpyDeviceToHost, st)) != hipSuccess) break;
+    if ((e = hipStreamSynchronize(st)) != hipSuccess) break;
+    // scatter the complete lists' results; a list past its capacity goes to the exact scan
+    std::vector<int64_t> done;
+    std::vector<int64_t> rows_ok;
+    for (int64_t j = 0; j < ng; ++j) {
+      if (hcnt[j] > cap_max) full.push_back(qs[g0 + j]);
+      else { done.push_back(qs[g0 + j]); rows_ok.push_back(j); }
+    }
+    if (done.size() == (size_t)ng) {
+      e = gather_rows(w + p_s, (int64_t)k * 4, gx, ng, (int64_t)k * 4, osc, (int64_t)k * 4, true, st);
+      if (e == hipSuccess) e = gather_rows(w + p_i, (int64_t)k * 8, gx, ng, (int64_t)k * 8, oix, (int64_t)k * 8, true, st);
+    } else {
+      for (size_t j = 0; j < done.size() && e == hipSuccess; ++j) {
+        e = hipMemcpyAsync(osc + done[j] * k, (float*)(w + p_s) + rows_ok[j] * k, (size_t)k * 4,
+                           hipMemcpyDeviceToDevice, st);
+        if (e == hipSuccess)
+          e = hipMemcpyAsync(oix + done[j] * k, (int64_t*)(w + p_i) + rows_ok[j] * k, (size_t)k * 8,
+                             hipMemcpyDeviceToDevice, st);
+      }
+    }
+    if (e == hipSuccess) e = hipStreamSynchronize(st);   // gx is rewritten by the next group
+  }
+  (void)hipStreamSynchronize(st);
+  (void)hipFree(w);
+  if (r) return r;
+  if (e != hipSuccess) return fail(CLM_E_HIP, std::string("overflow (wide): ") + hipGetErrorString(e));
+  return CLM_OK;
+}
+
 // Bounded search (large N), per block of queries:
 //  1. theta[q] <= the fp16-pass k-th best score of q:
 //     sampled (k <= 256, N >= 4S): the k-th best over a strided sample of S rows -- a subset
@@ -1465,7 +1550,7 @@ static int search_bounded(clm_index* x, bool sampled, int64_t S, const u16* q16,
   const size_t o_sc = sampled ? take((size_t)nqb * S * 4) : 0;
   const size_t o_ts = take((size_t)nqb * k * 4);
   const size_t o_ti = take((size_t)nqb * k * 8);
-  const size_t o_th = take((size_t)nqb * 4);
+  const size_t o_th = take((size_t)nq * 4);   // every query's threshold (the overflow pass reuses them)
   const size_t o_cnt = take((size_t)nqb * 4);
   const size_t o_cs = take((size_t)nqb * CAND_CAP * 4);
   const size_t o_ci = take((size_t)nqb * CAND_CAP * 8);
@@ -1480,7 +1565,7 @@ static int search_bounded(clm_index* x, bool sampled, int64_t S, const u16* q16,
   int64_t* ci = (int64_t*)(w + o_ci);
   const void* xrows = x->rows32 ? (const void*)x->rows32 : (const void*)x->rows;
   std::vector<int> hcnt;
-  std::vector<int64_t> overflow;
+  std::vector<int64_t> overflow, ocount;
   for (int64_t q0 = 0; q0 < nq; q0 += nqb) {
     const int64_t nb = std::min(nqb, nq - q0);
     if (sampled) {
@@ -1493,13 +1578,13 @@ static int search_bounded(clm_index* x, bool sampled, int64_t S, const u16* q16,
     } else {
       if ((r = search_scan(x, false, q16 + q0 * dim, qinv + q0, nullptr, nullptr, nb, k, ts, ti, st))) return r;
     }
-    KCHK(filter_thresholds(ts, k, nb, k, RESCORE_MARGIN, th, st));
+    KCHK(filter_thresholds(ts, k, nb, k, RESCORE_MARGIN, th + q0, st));
     HIPCHK(hipMemsetAsync(cnt, 0, (size_t)nb * 4, st));
     GemmArgs gf{};
     gf.A = q16 + q0 * dim; gf.lda = dim; gf.W = x->rows; gf.ldw = dim;
     gf.M = (int)nb; gf.N = (int)N; gf.K = dim;
     gf.rscale = qinv + q0; gf.cscale = x->inv;
-    gf.theta = th; gf.theta_ld = 1;
+    gf.theta = th + q0; gf.theta_ld = 1;
     gf.cnt = cnt; gf.cand_s = cs; gf.cand_i = ci; gf.cap = CAND_CAP; gf.base = x->offset;
     gf.m_fastest = 1;
     KCHK(gemm(false, EPI_FILTER, gf, st));
@@ -1509,40 +1594,54 @@ static int search_bounded(clm_index* x, bool sampled, int64_t S, const u16* q16,
     HIPCHK(hipMemcpyAsync(hcnt.data(), cnt, (size_t)nb * 4, hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
     for (int64_t i = 0; i < nb; ++i)
-      if (hcnt[i] > CAND_CAP) overflow.push_back(q0 + i);
+      if (hcnt[i] > CAND_CAP) {
+        overflow.push_back(q0 + i);
+        ocount.push_back(hcnt[i]);
+      }
   }
   x->search_stats[sampled ? 0 : 3] += nq - (int64_t)overflow.size();
-  if (!overflow.empty()) {   // rare: a candidate list beyond CAND_CAP (many near-ties); redo exactly
-    // all overflowed queries of the call in ONE exact scan (the index is streamed once per query
-    // block of search_scan, not once per query): gather their fp32 rows and norms, scan, scatter
-    x->search_stats[2] += (int64_t)overflow.size();
-    const int64_t no = (int64_t)overflow.size();
-    size_t o2 = 0;
-    auto take2 = [&](size_t bytes) { size_t o = o2; o2 = round_up(o2 + bytes, 256); return o; };
-    const size_t p_q = take2((size_t)no * dim * 4), p_n = take2((size_t)no * 8), p_s = take2((size_t)no * k * 4),
-                 p_i = take2((size_t)no * k * 8);
-    uint8_t* wo = nullptr;
-    if (hipMalloc(&wo, o2) != hipSuccess) { (void)hipGetLastError(); return fail(CLM_E_OOM, "overflow workspace"); }
-    float* gq = (float*)(wo + p_q);
-    double* gn = (double*)(wo + p_n);
-    float* gs = (float*)(wo + p_s);
-    int64_t* gi = (int64_t*)(wo + p_i);
-    hipError_t e = hipSuccess;
-    for (int64_t j = 0; j < no && e == hipSuccess; ++j) {
-      e = hipMemcpyAsync(gq + j * dim, q32 + overflow[j] * dim, (size_t)dim * 4, hipMemcpyDeviceToDevice, st);
-      if (e == hipSuccess) e = hipMemcpyAsync(gn + j, qn + overflow[j], 8, hipMemcpyDeviceToDevice, st);
+  if (overflow.empty()) return CLM_OK;
+  // Candidate lists beyond CAND_CAP (near-duplicate rows inside the window). Lists of up to
+  // (SORT_MAX / k) chunks are rebuilt whole by a second filter pass over just those queries and
+  // re-scored chunk-wise (overflow_wide); longer ones are redone by the exact scan, all of them in
+  // ONE scan (the index is streamed once per query block of search_scan, not once per query).
+  x->search_stats[2] += (int64_t)overflow.size();
+  std::vector<int64_t> wide, wcount, full;
+  for (size_t j = 0; j < overflow.size(); ++j) {
+    // headroom over the first pass's count: a different tile shape may round a score differently
+    const int64_t cap2 = ocount[j] + ocount[j] / 8 + 256;
+    if ((cap2 + RESCORE_WIDE_CHUNK - 1) / RESCORE_WIDE_CHUNK * k <= 8192) {
+      wide.push_back(overflow[j]);
+      wcount.push_back(cap2);
+    } else {
+      full.push_back(overflow[j]);
     }
-    r = e == hipSuccess ? search_scan(x, true, nullptr, nullptr, gq, gn, no, k, gs, gi, st)
-                        : fail(CLM_E_HIP, std::string("overflow gather: ") + hipGetErrorString(e));
-    for (int64_t j = 0; j < no && r == CLM_OK && e == hipSuccess; ++j) {
-      e = hipMemcpyAsync(osc + overflow[j] * k, gs + j * k, (size_t)k * 4, hipMemcpyDeviceToDevice, st);
-      if (e == hipSuccess) e = hipMemcpyAsync(oix + overflow[j] * k, gi + j * k, (size_t)k * 8, hipMemcpyDeviceToDevice, st);
-    }
-    (void)hipStreamSynchronize(st);
-    (void)hipFree(wo);
-    if (r) return r;
-    if (e != hipSuccess) return fail(CLM_E_HIP, std::string("overflow scatter: ") + hipGetErrorString(e));
   }
+  if (!wide.empty() && (r = overflow_wide(x, wide, wcount, q16, qinv, q32, qn, th, k, osc, oix, full, st))) return r;
+  if (full.empty()) return CLM_OK;
+  const int64_t no = (int64_t)full.size();
+  size_t o2 = 0;
+  auto take2 = [&](size_t bytes) { size_t o = o2; o2 = round_up(o2 + bytes, 256); return o; };
+  const size_t p_x = take2((size_t)no * 8), p_q = take2((size_t)no * dim * 4), p_n = take2((size_t)no * 8),
+               p_s = take2((size_t)no * k * 4), p_i = take2((size_t)no * k * 8);
+  uint8_t* wo = nullptr;
+  if (hipMalloc(&wo, o2) != hipSuccess) { (void)hipGetLastError(); return fail(CLM_E_OOM, "overflow workspace"); }
+  int64_t* gx = (int64_t*)(wo + p_x);
+  float* gq = (float*)(wo + p_q);
+  double* gn = (double*)(wo + p_n);
+  float* gs = (float*)(wo + p_s);
+  int64_t* gi = (int64_t*)(wo + p_i);
+  hipError_t e = hipMemcpyAsync(gx, full.data(), (size_t)no * 8, hipMemcpyHostToDevice, st);
+  if (e == hipSuccess) e = gather_rows(q32, (int64_t)dim * 4, gx, no, (int64_t)dim * 4, gq, (int64_t)dim * 4, false, st);
+  if (e == hipSuccess) e = gather_rows(qn, 8, gx, no, 8, gn, 8, false, st);
+  r = e == hipSuccess ? search_scan(x, true, nullptr, nullptr, gq, gn, no, k, gs, gi, st)
+                      : fail(CLM_E_HIP, std::string("overflow gather: ") + hipGetErrorString(e));
+  if (r == CLM_OK) e = gather_rows(gs, (int64_t)k * 4, gx, no, (int64_t)k * 4, osc, (int64_t)k * 4, true, st);
+  if (r == CLM_OK && e == hipSuccess) e = gather_rows(gi, (int64_t)k * 8, gx, no, (int64_t)k * 8, oix, (int64_t)k * 8, true, st);
+  (void)hipStreamSynchronize(st);
+  (void)hipFree(wo);
+  if (r) return r;
+  if (e != hipSuccess) return fail(CLM_E_HIP, std::string("overflow scatter: ") + hipGetErrorString(e));
   return CLM_OK;
 }
 

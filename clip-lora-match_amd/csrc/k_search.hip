@@ -21,6 +21,7 @@ namespace {
 constexpr int NT = 1024;
 constexpr int CAP = 4096;
 constexpr int SORT_MAX = 8192;
+constexpr int WIDE_CH = 4096;   // rescore_wide chunk (kernels.hpp RESCORE_WIDE_CHUNK)
 
 __device__ __forceinline__ uint32_t fkey(float f) {
   const uint32_t u = __float_as_uint(f);
@@ -309,6 +310,61 @@ __global__ __launch_bounds__(NT) void rescore_select_kernel(const float* cs, con
   }
 }
 
+// Overflowed candidate lists (more rows inside the window than CAND_CAP: near-duplicate rows)
+// are rebuilt by the host with a capacity that holds all of them and cut into chunks of WIDE_CH
+// candidates; per (chunk, query) one workgroup computes every candidate's exact score through
+// dot_wave / cos_from (the bits of every other path), sorts the chunk's (exact key, index) in
+// LDS and emits its top k (-inf / -1 padding); topk_merge_kernel then merges the chunks' lists.
+// The list holds the exact top-k of the index (as rescore_select's does), so the result is the
+// full exact scan's.
+template <typename R>
+__global__ __launch_bounds__(NT) void rescore_wide_kernel(const int64_t* ci, const int* cnt, int64_t cap,
+                                                          const float* q, const double* qn, int dim, const R* rows,
+                                                          int64_t offset, int k, int nch, float* os, int64_t* oi) {
+  __shared__ uint64_t keys[WIDE_CH];
+  const int64_t row = blockIdx.y;
+  const int ch = blockIdx.x;
+  const int64_t c = min((int64_t)cnt[row], cap);
+  const int64_t j0 = (int64_t)ch * WIDE_CH;
+  const int n = (int)max<int64_t>(0, min<int64_t>(c - j0, WIDE_CH));
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const float* qr = q + row * dim;
+  const double qnr = qn[row];
+  for (int j = wid; j < n; j += NT / 64) {
+    const int64_t gix = ci[row * cap + j0 + j];
+    double d, rr;
+    dot_wave(qr, rows + (gix - offset) * dim, dim, lane, d, rr);
+    const float sc = cos_from(d, qnr, rr);
+    if (lane == 0) keys[j] = ((uint64_t)fkey(sc) << 32) | (uint64_t)(0xFFFFFFFFu - (uint32_t)gix);
+  }
+  int n2 = 1;
+  while (n2 < n) n2 <<= 1;
+  for (int j = n + threadIdx.x; j < n2; j += NT) keys[j] = 0;
+  __syncthreads();
+  if (n2 > 1) bitonic_desc(keys, n2);
+  float* o_s = os + (row * nch + ch) * k;
+  int64_t* o_i = oi + (row * nch + ch) * k;
+  for (int j = threadIdx.x; j < k; j += NT) {
+    if (j < n) {
+      const uint64_t v = keys[j];
+      o_s[j] = kfloat((uint32_t)(v >> 32));
+      o_i[j] = (int64_t)(0xFFFFFFFFu - (uint32_t)(v & 0xFFFFFFFFu));
+    } else {
+      o_s[j] = -INFINITY;
+      o_i[j] = -1;
+    }
+  }
+}
+
+// row gather / scatter of `row_bytes` per row: dst[j] = src[idx[j]] (scatter: dst[idx[j]] = src[j])
+__global__ void gather_rows_kernel(const uint8_t* src, int64_t src_stride, const int64_t* idx, int64_t row_bytes,
+                                   uint8_t* dst, int64_t dst_stride, int scatter) {
+  const int64_t j = blockIdx.x, r = idx[j];
+  const uint8_t* sp = src + (scatter ? j : r) * src_stride;
+  uint8_t* dp = dst + (scatter ? r : j) * dst_stride;
+  for (int64_t b = threadIdx.x; b < row_bytes; b += blockDim.x) dp[b] = sp[b];
+}
+
 // filter threshold: th[q] = fp16-pass k-th score of q (ts[q * ld + k - 1]) - margin
 __global__ void theta_kernel(const float* ts, int64_t ld, int64_t nq, int k, float margin, float* th) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -391,6 +447,31 @@ hipError_t rescore_select(const float* cand_s, const int64_t* cand_i, const int*
   else
     rescore_select_kernel<float><<<(unsigned)nq, NT, 0, s>>>(cand_s, cand_i, cnt, cap, q, qn, dim,
                                                              (const float*)rows, offset, margin, k, out_s, out_i);
+  return hipGetLastError();
+}
+
+hipError_t rescore_wide(const int64_t* cand_i, const int* cnt, int64_t cap, const float* q, const double* qn, int dim,
+                        const void* rows, bool rows_f16, int64_t offset, int64_t nq, int k, float* part_s,
+                        int64_t* part_i, hipStream_t s) {
+  static_assert(WIDE_CH == RESCORE_WIDE_CHUNK, "chunk size");
+  if (nq <= 0) return hipSuccess;
+  const int64_t nch = (cap + WIDE_CH - 1) / WIDE_CH;
+  if (k < 1 || k > WIDE_CH || nch < 1 || nch * k > SORT_MAX || nq > 65535) return hipErrorInvalidValue;
+  const dim3 grid((unsigned)nch, (unsigned)nq);
+  if (rows_f16)
+    rescore_wide_kernel<u16><<<grid, NT, 0, s>>>(cand_i, cnt, cap, q, qn, dim, (const u16*)rows, offset, k, (int)nch,
+                                                 part_s, part_i);
+  else
+    rescore_wide_kernel<float><<<grid, NT, 0, s>>>(cand_i, cnt, cap, q, qn, dim, (const float*)rows, offset, k,
+                                                   (int)nch, part_s, part_i);
+  return hipGetLastError();
+}
+
+hipError_t gather_rows(const void* src, int64_t src_stride, const int64_t* idx, int64_t n, int64_t row_bytes,
+                       void* dst, int64_t dst_stride, bool scatter, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  gather_rows_kernel<<<(unsigned)n, 256, 0, s>>>((const uint8_t*)src, src_stride, idx, row_bytes, (uint8_t*)dst,
+                                                 dst_stride, scatter ? 1 : 0);
   return hipGetLastError();
 }
 

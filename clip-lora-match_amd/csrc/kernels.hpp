@@ -184,6 +184,16 @@ hipError_t exact_scores(const float* q, const double* qn, int64_t nq, const void
 hipError_t rescore_select(const float* cand_s, const int64_t* cand_i, const int* cnt, int cap, const float* q,
                           const double* qn, int dim, const void* rows, bool rows_f16, int64_t offset, float margin,
                           int64_t nq, int k, float* out_s, int64_t* out_i, hipStream_t s);
+// overflowed lists: candidates [nq, cap] (global indices; cnt[q] <= cap) -> per chunk of
+// RESCORE_WIDE_CHUNK candidates the top k by (exact score desc, index asc), part_s / part_i
+// [nq, ceil(cap / chunk) * k] (-inf / -1 padded), merged by topk_merge; ceil(cap / chunk) * k <= 8192
+constexpr int RESCORE_WIDE_CHUNK = 4096;
+hipError_t rescore_wide(const int64_t* cand_i, const int* cnt, int64_t cap, const float* q, const double* qn, int dim,
+                        const void* rows, bool rows_f16, int64_t offset, int64_t nq, int k, float* part_s,
+                        int64_t* part_i, hipStream_t s);
+// dst row j = src row idx[j] (scatter: dst row idx[j] = src row j), row_bytes per row
+hipError_t gather_rows(const void* src, int64_t src_stride, const int64_t* idx, int64_t n, int64_t row_bytes,
+                       void* dst, int64_t dst_stride, bool scatter, hipStream_t s);
 // th[q] = ts[q * ld + k - 1] - margin
 hipError_t filter_thresholds(const float* ts, int64_t ld, int64_t nq, int k, float margin, float* th, hipStream_t s);
 

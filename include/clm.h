@@ -180,7 +180,8 @@ int clm_index_search(clm_index* idx, const void* q, int q_dtype, int64_t nq, int
 
 /* search-path counters since creation: queries served by the sampled single-pass bounded
  * search (`filtered`), by the exact scan or the fp16-scan-bounded search (`exact`), and
- * bounded queries redone by the exact scan after a candidate-list overflow */
+ * bounded queries whose candidate list overflowed (redone by a whole-list pass, or by the exact
+ * scan when the list is longer than 8192 / k chunks of 4096) */
 int clm_index_stats(const clm_index* idx, int64_t* filtered, int64_t* exact, int64_t* overflow);
 /* out[0..n): sampled bounded, fp16-scan bounded, full exact scan, overflow re-runs */
 int clm_index_stats2(const clm_index* idx, int64_t* out, int n);

@@ -320,6 +320,30 @@ def test_many_overflowing_queries_one_exact_rescan(monkeypatch):
     idx.close()
 
 
+@pytest.mark.parametrize("k", [1, 8, 1024])
+def test_overflow_wide_and_exact_paths(monkeypatch, k):
+    """Overflowed lists are rebuilt whole and re-scored chunk-wise when ceil(list / 4096) * k <=
+    8192 (k = 1, 8: tie groups of 60k rows), else redone by the exact scan (k = 1024); both agree
+    bit for bit with the full exact scan, including the random queries of the same block."""
+    monkeypatch.setenv("CLM_SEARCH_BOUNDED", "1")
+    n, dim = 300_000, 96
+    g = torch.Generator(device="cuda").manual_seed(11)
+    rows = torch.randn((n, dim), generator=g, device="cuda")
+    dups = torch.randn((2, dim), generator=g, device="cuda")
+    rows[10_000:70_000] = dups[0] + 1e-3 * torch.randn((60_000, dim), generator=g, device="cuda")
+    rows[200_000:205_000] = dups[1] + 1e-3 * torch.randn((5_000, dim), generator=g, device="cuda")
+    idx = CosineIndex(dim, capacity=n)
+    idx.append(rows.half())
+    q = torch.cat([dups.repeat(3, 1), torch.randn((5, dim), generator=g, device="cuda")]).half()
+    s, i = idx.search(q, k)
+    assert idx.stats()["overflow"] >= 3
+    monkeypatch.delenv("CLM_SEARCH_BOUNDED")
+    monkeypatch.setenv("CLM_SEARCH_FULL", "1")
+    s_ref, i_ref = idx.search(q, k)
+    assert torch.equal(i, i_ref) and torch.equal(s, s_ref)
+    idx.close()
+
+
 # ---- query fusion (seeker_service.py:84-186) ------------------------------------------------
 def _unit_rows(n, d, seed):
     x = np.random.default_rng(seed).standard_normal((n, d)).astype(np.float32)
