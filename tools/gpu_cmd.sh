@@ -1,5 +1,5 @@
 #!/bin/bash
-# scratch GPU session script (the command of the last gpurun call)
+# scratch GPU session script (the command of the last gpurun call): the GPU test suite and smoke
 cd "$(dirname "$0")/.." && export TMPDIR=/tmp && mkdir -p gpurun_out
-DO_TEST=0 DO_PROF=1 bash tools/gpu_r03.sh || exit 1
-DO_TEST=0 DO_BENCH=1 bash tools/gpu_r03.sh || exit 1
+timeout -k 10 600 python -u -m pytest tests -m gpu -q -x --timeout 300 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1; rc=$?; echo "pytest rc=$rc"; tail -3 gpurun_out/pytest_gpu.log; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1; rc=$?; echo "smoke rc=$rc"; tail -1 gpurun_out/smoke.log; exit $rc
