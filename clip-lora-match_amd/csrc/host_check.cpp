@@ -135,6 +135,46 @@ static void device_checks() {
   CHECK(ix[0] == -1 && std::isinf(sc[0]));   // empty index: (-inf, -1) slots
   CHECK(clm_index_destroy(idx) == CLM_OK);
 
+  // near-duplicate rows: 3000 copies of one row (and 3000 others) overflow the bounded path's
+  // 2048-candidate lists; those queries take the whole-list pass (overflow_wide), k = 7 and 1024
+  {
+    const int nd = 6000, ndup = 3000, nqd = 4;
+    std::vector<float> drows((size_t)nd * dim);
+    for (auto& v : drows) v = frand();
+    for (int j = 1; j < ndup; ++j) std::memcpy(&drows[(size_t)(2 * j) * dim], &drows[0], dim * 4);   // even rows
+    clm_index* di = nullptr;
+    CHECK(clm_index_create(0, nd, dim, &di) == CLM_OK);
+    if (di) {
+      CHECK(clm_index_append(di, drows.data(), CLM_F32, nd, nullptr) == CLM_OK);
+      std::vector<float> dq((size_t)nqd * dim);
+      for (auto& v : dq) v = frand();
+      std::memcpy(dq.data(), drows.data(), dim * 4);
+      std::memcpy(dq.data() + 2 * dim, drows.data(), dim * 4);
+      setenv("CLM_SEARCH_BOUNDED", "1", 1);
+      for (int kk : {7, 1024}) {
+        int64_t s0[4] = {0, 0, 0, 0}, s1[4] = {0, 0, 0, 0};
+        CHECK(clm_index_stats2(di, s0, 4) == CLM_OK);
+        std::vector<float> dsc((size_t)nqd * kk);
+        std::vector<int64_t> dix((size_t)nqd * kk);
+        CHECK(clm_index_search(di, dq.data(), CLM_F32, nqd, kk, dsc.data(), dix.data(), nullptr) == CLM_OK);
+        CHECK(clm_index_stats2(di, s1, 4) == CLM_OK && s1[3] - s0[3] >= 2);   // the two duplicate queries
+        for (int i = 0; i < nqd; ++i) {
+          std::vector<std::pair<double, int64_t>> all(nd);
+          for (int j = 0; j < nd; ++j) all[j] = {cos64(&dq[(size_t)i * dim], &drows[(size_t)j * dim], dim), j};
+          std::partial_sort(all.begin(), all.begin() + kk, all.end(), [](const auto& a, const auto& b) {
+            return a.first > b.first || (a.first == b.first && a.second < b.second);
+          });
+          for (int t = 0; t < kk; ++t) {
+            CHECK(dix[(size_t)i * kk + t] == all[t].second);
+            CHECK(dsc[(size_t)i * kk + t] == (float)all[t].first);
+          }
+        }
+      }
+      unsetenv("CLM_SEARCH_BOUNDED");
+      CHECK(clm_index_destroy(di) == CLM_OK);
+    }
+  }
+
   // exact cosine matrix on host buffers, any dim
   const int cd = 77, cn = 33;
   std::vector<float> cq((size_t)nq * cd), cc((size_t)cn * cd), cout((size_t)nq * cn);
