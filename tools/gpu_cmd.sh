@@ -1,6 +1,5 @@
 #!/bin/bash
-# scratch GPU session script (the command of the last gpurun call)
+# scratch GPU session script (the command of the last gpurun call): the GPU test suite and smoke
 cd "$(dirname "$0")/.." && export TMPDIR=/tmp && mkdir -p gpurun_out
-cp ab/libclm_B.so clip-lora-match_amd/libclm.so
-timeout -k 10 400 python -u -m pytest tests/test_gpu_encode.py -x -q --timeout 300 --timeout-method thread > gpurun_out/t8.log 2>&1; rc=$?; tail -2 gpurun_out/t8.log; [ $rc -eq 0 ] || exit $rc
-ARMS="A=A F=B" bash tools/ab_lib.sh || exit 1
+timeout -k 10 600 python -u -m pytest tests -m gpu -q -x --timeout 300 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1; rc=$?; echo "pytest rc=$rc"; tail -3 gpurun_out/pytest_gpu.log; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1; rc=$?; echo "smoke rc=$rc"; tail -1 gpurun_out/smoke.log; exit $rc
