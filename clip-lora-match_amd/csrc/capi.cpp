@@ -16,6 +16,7 @@
 #include <algorithm>
 #include <cmath>
 #include <map>
+#include <mutex>
 #include <tuple>
 #include <cstdlib>
 #include <cstring>
@@ -212,6 +213,8 @@ struct clm_index {
   void* ws = nullptr; size_t ws_bytes = 0;
   void* ws2 = nullptr; size_t ws2_bytes = 0;
   void* ws3 = nullptr; size_t ws3_bytes = 0;
+  // ws4 = the overflow passes' gathered queries / candidate lists (overflow_wide, exact re-scan)
+  void* ws4 = nullptr; size_t ws4_bytes = 0;
   // strided row sample for the threshold pass, rebuilt when n changes
   u16* samp = nullptr; float* samp_inv = nullptr; int64_t samp_S = 0, samp_n = -1, samp_cap = 0;
   // queries served by: [0] sampled bounded search, [1] the full exact scan, [2] overflow re-runs,
@@ -638,7 +641,7 @@ int run_layers(clm_ctx* c, Tower& T, int B, int S, bool causal, const int32_t* i
     g.A = T.X; g.lda = T.ldx; g.M = (int)M; g.N = T.mlp; g.K = Lw.k_fc1; g.out = T.Hm; g.ldo = T.ldm;
     g.W = Lw.w_fc1; g.ldw = Lw.k_fc1; g.bias = Lw.b_fc1;
     if (!pooled) g.m_dev = mdev;
-    { PROF(CLM_PROF_GEMM, 2.0 * (pooled ? (double)M : Mx) * g.N * g.K);   // pooled rows: 64 x 128 tiles fill the chip
+    { PROF(CLM_PROF_GEMM, 2.0 * (pooled ? (double)M : Mx) * g.N * g.K);   // pooled rows: 128 x 64 tiles (4 waves) fill the chip
       KCHK(pooled ? gemm_cfg(bf, EPI_GELU, GEMM_CFG_SPLITK, g, st) : gemm(bf, EPI_GELU, g, st)); }
     if (Lw.r_fc2) { PROF(CLM_PROF_OTHER, 2.0 * M * T.mlp + 4.0 * Lw.r_fc2 * T.mlp);
       KCHK(lora_down(bf, T.Hm, T.ldm, (int)M, T.mlp, Lw.a_fc2, Lw.r_fc2, RPAD, st)); }
@@ -1145,7 +1148,7 @@ int clm_index_destroy(clm_index* x) {
   if (!x) return CLM_OK;
   DeviceGuard g(x->dev);
   (void)hipDeviceSynchronize();
-  for (void* p : {(void*)x->rows, (void*)x->inv, (void*)x->rows32, x->ws, x->ws2, x->ws3, (void*)x->samp,
+  for (void* p : {(void*)x->rows, (void*)x->inv, (void*)x->rows32, x->ws, x->ws2, x->ws3, x->ws4, (void*)x->samp,
                   (void*)x->samp_inv})
     if (p) (void)hipFree(p);
   delete x;
@@ -1348,6 +1351,23 @@ static int grow(void** p, size_t* cap, size_t bytes) {
   return CLM_OK;
 }
 
+// Grow-only per-device scratch for the entry points that stage host buffers (resize_crop,
+// cosine_scores, topk_merge, l2_normalize, fuse_queries): no hipMalloc / hipFree per call -- hipFree
+// synchronises the whole device, which stalled work queued on other streams (the concurrent tower
+// stream) behind a single-image encode. A caller holds the device's lock until its stream has
+// drained the scratch (every such entry point synchronises its stream before returning).
+struct Scratch {
+  std::mutex mu;
+  void* p = nullptr;
+  size_t bytes = 0;
+};
+static Scratch& scratch_of_current_device() {
+  static Scratch s[64];
+  int d = 0;
+  if (hipGetDevice(&d) != hipSuccess) { (void)hipGetLastError(); d = 0; }
+  return s[d & 63];
+}
+
 // The MFMA pass scores fp16 unit-rounded operands: |fp16-pass score - exact cosine| <= 2.05e-3
 // (each side's rounding moves a cosine by <= 2u, u = 2^-11, plus fp32 accumulation of <= 1024
 // products). Every row of the exact top-k therefore has an fp16-pass score within 2 x 2.05e-3 of
@@ -1435,8 +1455,8 @@ static int overflow_wide(clm_index* x, const std::vector<int64_t>& qs, const std
                p_cnt = take((size_t)G * 4), p_cs = take((size_t)G * cap_max * 4), p_ci = take((size_t)G * cap_max * 8),
                p_ps = take((size_t)G * nch * k * 4), p_pi = take((size_t)G * nch * k * 8),
                p_s = take((size_t)G * k * 4), p_i = take((size_t)G * k * 8);
-  uint8_t* w = nullptr;
-  if (hipMalloc(&w, off) != hipSuccess) { (void)hipGetLastError(); return fail(CLM_E_OOM, "overflow workspace"); }
+  if (int rg = grow(&x->ws4, &x->ws4_bytes, off)) return rg;
+  uint8_t* w = (uint8_t*)x->ws4;
   int64_t* gx = (int64_t*)(w + p_x);
   int* cnt = (int*)(w + p_cnt);
   std::vector<int> hcnt;
@@ -1490,7 +1510,6 @@ static int overflow_wide(clm_index* x, const std::vector<int64_t>& qs, const std
     if (e == hipSuccess) e = hipStreamSynchronize(st);   // gx is rewritten by the next group
   }
   (void)hipStreamSynchronize(st);
-  (void)hipFree(w);
   if (r) return r;
   if (e != hipSuccess) return fail(CLM_E_HIP, std::string("overflow (wide): ") + hipGetErrorString(e));
   return CLM_OK;
@@ -1624,8 +1643,8 @@ static int search_bounded(clm_index* x, bool sampled, int64_t S, const u16* q16,
   auto take2 = [&](size_t bytes) { size_t o = o2; o2 = round_up(o2 + bytes, 256); return o; };
   const size_t p_x = take2((size_t)no * 8), p_q = take2((size_t)no * dim * 4), p_n = take2((size_t)no * 8),
                p_s = take2((size_t)no * k * 4), p_i = take2((size_t)no * k * 8);
-  uint8_t* wo = nullptr;
-  if (hipMalloc(&wo, o2) != hipSuccess) { (void)hipGetLastError(); return fail(CLM_E_OOM, "overflow workspace"); }
+  if ((r = grow(&x->ws4, &x->ws4_bytes, o2))) return r;   // overflow_wide is done with it (it drains its stream)
+  uint8_t* wo = (uint8_t*)x->ws4;
   int64_t* gx = (int64_t*)(wo + p_x);
   float* gq = (float*)(wo + p_q);
   double* gn = (double*)(wo + p_n);
@@ -1639,7 +1658,6 @@ static int search_bounded(clm_index* x, bool sampled, int64_t S, const u16* q16,
   if (r == CLM_OK) e = gather_rows(gs, (int64_t)k * 4, gx, no, (int64_t)k * 4, osc, (int64_t)k * 4, true, st);
   if (r == CLM_OK && e == hipSuccess) e = gather_rows(gi, (int64_t)k * 8, gx, no, (int64_t)k * 8, oix, (int64_t)k * 8, true, st);
   (void)hipStreamSynchronize(st);
-  (void)hipFree(wo);
   if (r) return r;
   if (e != hipSuccess) return fail(CLM_E_HIP, std::string("overflow scatter: ") + hipGetErrorString(e));
   return CLM_OK;
@@ -1745,8 +1763,10 @@ int clm_cosine_scores(int hip_device, const float* q, int64_t nq, const float* c
   const bool qd = is_device_ptr(q), cd = is_device_ptr(c), od = is_device_ptr(out);
   size_t bytes = (size_t)nq * 8 + (qd ? 0 : (size_t)nq * dim * 4) + (cd ? 0 : (size_t)n * dim * 4) +
                  (od ? 0 : (size_t)nq * n * 4) + 1024;
-  uint8_t* w = nullptr;
-  if (hipMalloc(&w, bytes) != hipSuccess) { (void)hipGetLastError(); return fail(CLM_E_OOM, "workspace"); }
+  Scratch& scr = scratch_of_current_device();
+  std::lock_guard<std::mutex> lock(scr.mu);
+  if (int rg = grow(&scr.p, &scr.bytes, bytes)) return rg;
+  uint8_t* w = (uint8_t*)scr.p;
   size_t off = 0;
   auto take = [&](size_t b) { size_t o = off; off = round_up(off + b, 256); return w + o; };
   double* qn = (double*)take((size_t)nq * 8);
@@ -1763,7 +1783,6 @@ int clm_cosine_scores(int hip_device, const float* q, int64_t nq, const float* c
   if (e == hipSuccess && !od) e = hipMemcpyAsync(out, os, (size_t)nq * n * 4, hipMemcpyDeviceToHost, st);
   if (e == hipSuccess) e = hipStreamSynchronize(st);
   if (e != hipSuccess) rc = fail(CLM_E_HIP, std::string("cosine_scores: ") + hipGetErrorString(e));
-  (void)hipFree(w);
   return rc;
 }
 
@@ -1782,7 +1801,13 @@ int clm_topk_merge(int hip_device, const float* scores, const int64_t* idx, int6
   // +512 slack under-allocated 4 small takes -- found by the host-sanitizer harness)
   const size_t bytes = (in_d ? 0 : round_up(n_in * 4, 256) + round_up(n_in * 8, 256)) +
                        (out_d ? 0 : round_up((size_t)nq * k * 4, 256) + round_up((size_t)nq * k * 8, 256));
-  if (bytes > 0 && hipMalloc(&w, bytes) != hipSuccess) { (void)hipGetLastError(); return fail(CLM_E_OOM, "workspace"); }
+  Scratch& scr = scratch_of_current_device();
+  std::unique_lock<std::mutex> lock(scr.mu, std::defer_lock);
+  if (bytes > 0) {   // host lists: staged through the device scratch (the call drains its stream)
+    lock.lock();
+    if (int rg = grow(&scr.p, &scr.bytes, bytes)) return rg;
+    w = (uint8_t*)scr.p;
+  }
   size_t off = 0;
   auto take = [&](size_t b) { size_t o = off; off = round_up(off + b, 256); return w + o; };
   const float* s_in = scores;
@@ -1804,7 +1829,6 @@ int clm_topk_merge(int hip_device, const float* scores, const int64_t* idx, int6
     if (e == hipSuccess) e = hipMemcpyAsync(out_idx, i_out, (size_t)nq * k * 8, hipMemcpyDeviceToHost, st);
   }
   if (e == hipSuccess && (!in_d || !out_d)) e = hipStreamSynchronize(st);
-  if (w) (void)hipFree(w);
   if (e != hipSuccess) return fail(CLM_E_HIP, std::string("topk_merge: ") + hipGetErrorString(e));
   return CLM_OK;
 }
@@ -1818,13 +1842,14 @@ int clm_l2_normalize(int hip_device, float* rows, int64_t n, int dim, void* stre
     KCHK(l2_normalize_rows(rows, n, dim, st));
     return CLM_OK;
   }
-  float* t = nullptr;
-  if (hipMalloc(&t, (size_t)n * dim * 4) != hipSuccess) { (void)hipGetLastError(); return fail(CLM_E_OOM, "workspace"); }
+  Scratch& scr = scratch_of_current_device();
+  std::lock_guard<std::mutex> lock(scr.mu);
+  if (int rg = grow(&scr.p, &scr.bytes, (size_t)n * dim * 4)) return rg;
+  float* t = (float*)scr.p;
   hipError_t e = hipMemcpyAsync(t, rows, (size_t)n * dim * 4, hipMemcpyHostToDevice, st);
   if (e == hipSuccess) e = l2_normalize_rows(t, n, dim, st);
   if (e == hipSuccess) e = hipMemcpyAsync(rows, t, (size_t)n * dim * 4, hipMemcpyDeviceToHost, st);
   if (e == hipSuccess) e = hipStreamSynchronize(st);
-  (void)hipFree(t);
   if (e != hipSuccess) return fail(CLM_E_HIP, std::string("l2_normalize: ") + hipGetErrorString(e));
   return CLM_OK;
 }
@@ -1843,15 +1868,16 @@ int clm_fuse_queries(int hip_device, const float* a, float w_a, const float* b, 
     return CLM_OK;
   }
   const size_t bytes = (size_t)n * dim * 4;
-  float* t = nullptr;
-  if (hipMalloc(&t, bytes * (b ? 2 : 1)) != hipSuccess) { (void)hipGetLastError(); return fail(CLM_E_OOM, "workspace"); }
+  Scratch& scr = scratch_of_current_device();
+  std::lock_guard<std::mutex> lock(scr.mu);
+  if (int rg = grow(&scr.p, &scr.bytes, bytes * (b ? 2 : 1))) return rg;
+  float* t = (float*)scr.p;
   float* tb = b ? t + (size_t)n * dim : nullptr;
   hipError_t e = hipMemcpyAsync(t, a, bytes, hipMemcpyHostToDevice, st);
   if (e == hipSuccess && b) e = hipMemcpyAsync(tb, b, bytes, hipMemcpyHostToDevice, st);
   if (e == hipSuccess) e = fuse_rows(t, w_a, tb, w_b, n, dim, t, st);
   if (e == hipSuccess) e = hipMemcpyAsync(out, t, bytes, hipMemcpyDeviceToHost, st);
   if (e == hipSuccess) e = hipStreamSynchronize(st);
-  (void)hipFree(t);
   if (e != hipSuccess) return fail(CLM_E_HIP, std::string("fuse_queries: ") + hipGetErrorString(e));
   return CLM_OK;
 }
@@ -1929,7 +1955,12 @@ extern "C" int clm_resize_crop(int hip_device, const uint8_t* src, const int64_t
     src_bytes = std::max(src_bytes, offs[i] + (int64_t)H * W * 3);
     // get_resize_output_image_size(default_to_square=False): short -> S, long -> int(S * long / short)
     const int shrt = std::min(H, W), lng = std::max(H, W);
-    const int new_long = (int)((double)((int64_t)S * lng) / shrt);
+    // int(S * long / short) in double as transformers does; an extreme aspect ratio (a 1 x 10^7
+    // strip) would overflow int -- undefined behaviour, PIL fails on it too: refuse
+    const double nl = (double)((int64_t)S * lng) / shrt;
+    if (!(nl < (double)(1 << 24)))
+      return fail(CLM_E_ARG, "resize_crop: image " + std::to_string(i) + " resizes to a side over 2^24 pixels");
+    const int new_long = (int)nl;
     const int nh = W <= H ? new_long : S, nw = W <= H ? S : new_long;
     const int top = (nh - S) / 2, left = (nw - S) / 2;   // center_crop; nh, nw >= S
     ResizeDesc& d = desc[i];
@@ -1962,8 +1993,10 @@ extern "C" int clm_resize_crop(int hip_device, const uint8_t* src, const int64_t
   const size_t b_desc = round_up(sizeof(ResizeDesc) * n, 256), b_coef = round_up(coef.size() * 4, 256);
   const size_t bytes = b_desc + b_coef + (size_t)tmp_bytes + (sd ? 0 : round_up(src_bytes, 256)) +
                        (od ? 0 : round_up(out_bytes, 256));
-  uint8_t* w = nullptr;
-  if (hipMalloc(&w, bytes) != hipSuccess) { (void)hipGetLastError(); return fail(CLM_E_OOM, "resize_crop workspace"); }
+  Scratch& scr = scratch_of_current_device();
+  std::lock_guard<std::mutex> lock(scr.mu);
+  if (int rg = grow(&scr.p, &scr.bytes, bytes)) return rg;
+  uint8_t* w = (uint8_t*)scr.p;
   size_t off = 0;
   auto take = [&](size_t b) { size_t o = off; off = round_up(off + b, 256); return w + o; };
   ResizeDesc* d_desc = (ResizeDesc*)take(sizeof(ResizeDesc) * n);
@@ -1983,7 +2016,6 @@ extern "C" int clm_resize_crop(int hip_device, const uint8_t* src, const int64_t
   if (e == hipSuccess && !od) e = hipMemcpyAsync(out, d_out, out_bytes, hipMemcpyDeviceToHost, st);
   // the tables live in host vectors and the workspace is freed below: wait for the stream
   if (e == hipSuccess) e = hipStreamSynchronize(st);
-  (void)hipFree(w);
   if (e != hipSuccess) return fail(CLM_E_HIP, std::string("resize_crop: ") + hipGetErrorString(e));
   return CLM_OK;
 }

@@ -48,7 +48,7 @@ hipError_t gemm_splitk_resid(bool bf16, const GemmArgs& g, int slices, float* ws
 // fp32 workspace bytes gemm_splitk_resid needs
 inline size_t gemm_splitk_ws_bytes(int M, int N, int slices) { return (size_t)slices * M * N * 4; }
 // explicit tile configuration (config < 0: heuristic); configs: k_gemm.hip launch_id.
-// GEMM_CFG_SPLITK: the 64 x 128 tile, for few-row GEMMs (the pooled last layer)
+// GEMM_CFG_SPLITK: the 128 x 64 tile (4 waves), for few-row GEMMs (the pooled last layer)
 constexpr int GEMM_CFG_SPLITK = 2;
 hipError_t gemm_cfg(bool bf16, int epi, int config, const GemmArgs& g, hipStream_t s);
 int gemm_num_configs();

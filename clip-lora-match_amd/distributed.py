@@ -113,13 +113,19 @@ class ShardedIndex:
 
 
 def build_index_sharded(encode_rows: Callable[[int, int], torch.Tensor], n_total: int, batch: int,
-                        group=None) -> torch.Tensor:
+                        group=None, exchange: Optional[Callable[[torch.Tensor], torch.Tensor]] = None,
+                        restore: Optional[Callable[[torch.Tensor], torch.Tensor]] = None) -> torch.Tensor:
     """Index build over N GPUs: encode_rows(start, stop) encodes global rows [start, stop)
     (e.g. a slice of images or captions) on this rank's GPU; returns all n_total embeddings
-    on every rank (one all_gather)."""
+    on every rank (one all_gather). exchange / restore (optional) map the local rows to the form
+    that crosses the links and the gathered rows back (index_build's fp16 exchange: half the
+    bytes of the fp32 rows)."""
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
     start, stop = shard_range(n_total, rank, world)
     outs = [encode_rows(s, min(s + batch, stop)) for s in range(start, stop, batch)]
     local = torch.cat(outs, 0) if outs else encode_rows(start, start)   # [0, D] for an empty shard
-    return all_gather_rows(local, n_total, group)
+    if exchange is not None:
+        local = exchange(local)
+    rows = all_gather_rows(local, n_total, group)
+    return restore(rows) if restore is not None else rows

@@ -20,6 +20,7 @@ from __future__ import annotations
 
 import ctypes
 import os
+import threading
 from pathlib import Path
 from typing import List, Optional, Sequence, Union
 
@@ -42,6 +43,8 @@ class ClipProcessor:
         self.mean = cfg.mean
         self.std = cfg.std
         self._hf_image = None
+        self._pin = None                     # pinned staging of images_u8 (grow-only)
+        self._pin_lock = threading.Lock()
         self.tokenizer = None
         tdir = tokenizer_dir or os.environ.get("CLM_TOKENIZER_DIR")
         if tdir and Path(tdir, "vocab.json").exists() and Path(tdir, "merges.txt").exists():
@@ -84,17 +87,23 @@ class ClipProcessor:
         sizes = np.array([a.shape[0] * a.shape[1] * 3 for a in arrs], np.int64)
         offs = np.zeros(len(arrs), np.int64)
         offs[1:] = np.cumsum(sizes)[:-1]
-        flat = torch.empty(int(sizes.sum()), dtype=torch.uint8, pin_memory=True)
-        fv = flat.numpy()
-        for a, o, n in zip(arrs, offs, sizes):
-            fv[o:o + n] = a.reshape(-1)
-        src = flat.to(device, non_blocking=True)
+        total = int(sizes.sum())
         hw = np.array([a.shape[:2] for a in arrs], np.int32).reshape(-1)
         out = torch.empty((len(arrs), S, S, 3), dtype=torch.uint8, device=device)
-        _capi.check(_capi.lib().clm_resize_crop(
-            device.index if device.index is not None else torch.cuda.current_device(), _capi.ptr(src),
-            offs.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)), hw.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)),
-            len(arrs), S, _capi.ptr(out), _capi.stream_of(device)), "resize_crop")
+        # one grow-only pinned staging buffer per processor (no pinned allocation per
+        # call); it is free again when clm_resize_crop returns (that call drains the stream)
+        with self._pin_lock:
+            if self._pin is None or self._pin.numel() < total:
+                self._pin = torch.empty(max(total, 1 << 20), dtype=torch.uint8, pin_memory=True)
+            flat = self._pin[:total]
+            fv = flat.numpy()
+            for a, o, n in zip(arrs, offs, sizes):
+                fv[o:o + n] = a.reshape(-1)
+            src = flat.to(device, non_blocking=True)
+            _capi.check(_capi.lib().clm_resize_crop(
+                device.index if device.index is not None else torch.cuda.current_device(), _capi.ptr(src),
+                offs.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)), hw.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)),
+                len(arrs), S, _capi.ptr(out), _capi.stream_of(device)), "resize_crop")
         return out
 
     def normalize_lut(self) -> np.ndarray:

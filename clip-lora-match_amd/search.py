@@ -380,12 +380,15 @@ class TextSearchIndex:
         self = cls.__new__(cls)
         n, dim, dim_p = header["n"], header["dim"], header["dim_p"]
         _, secs = read_shard_header(path)
-        if header["has_f32"]:   # the host mirror: the fp32 rows, paged in lazily (copy-on-write map)
-            host = np.memmap(path, dtype=np.float32, mode="c", offset=secs["rows32"][0], shape=(n, dim_p))
+        if n == 0:   # an empty index has no data sections to map (mmap refuses 0 bytes at EOF)
+            host = torch.empty((0, dim), dtype=torch.float32)
         else:
-            host = np.memmap(path, dtype=np.float16, mode="r", offset=secs["rows16"][0], shape=(n, dim_p))
-        host = torch.from_numpy(np.ascontiguousarray(host[:, :dim]) if dim != dim_p or not header["has_f32"]
-                                else host).float()
+            if header["has_f32"]:   # the host mirror: the fp32 rows, paged in lazily (copy-on-write map)
+                host = np.memmap(path, dtype=np.float32, mode="c", offset=secs["rows32"][0], shape=(n, dim_p))
+            else:
+                host = np.memmap(path, dtype=np.float16, mode="r", offset=secs["rows16"][0], shape=(n, dim_p))
+            host = torch.from_numpy(np.ascontiguousarray(host[:, :dim]) if dim != dim_p or not header["has_f32"]
+                                    else host).float()
         self._host, self._n = host, n
         self.image_paths = list(header["meta"].get("image_paths", []))
         self.texts = list(header["meta"].get("texts", []))

@@ -1,0 +1,68 @@
+"""Worker of tests/test_gpu_distributed.py::test_index_build_1m_*: BASELINE configs[2] at its
+stated size -- rebuild_index(from_images=True) over 1,000,000 device-generated 224^2 images
+(synthetic.DeviceImages, pixels a function of the global row), ViT-B/32 + LoRA, fp16, batch 512,
+with the fp16 all_gather exchange -- at whatever world size torch.distributed.run started (gloo:
+the 1-GPU box rehearses world 2 on one device). Rank 0 reloads the .pt and writes a JSON verdict:
+the fold checksum of the returned rows and of the file, rows, and spot-checked image paths."""
+import json
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+
+import clip_lora_match_amd as clm  # noqa: E402
+from clip_lora_match_amd import synthetic as syn  # noqa: E402
+from clip_lora_match_amd import weights as W  # noqa: E402
+from clip_lora_match_amd.engine import ClipLoraModel  # noqa: E402
+from clip_lora_match_amd.index_build import fold_sha256, rebuild_index  # noqa: E402
+from clip_lora_match_amd.processor import ClipProcessor  # noqa: E402
+
+
+def main(out_path, tmpdir, n, exchange):
+    torch.cuda.set_device(0)
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world > 1:
+        dist.init_process_group("gloo")
+    rank = dist.get_rank() if world > 1 else 0
+    cfg = clm.get_preset("ViT-B/32")
+    model = ClipLoraModel(cfg, compute_dtype="float16", max_batch=512)
+    model.load_tensors(W.synthetic_state_dict(cfg, 0))
+    model.load_tensors(W.synthetic_lora(cfg, 1))
+    model.finalize()
+    src = syn.DeviceImages(n, cfg.image_size, seed=20240)
+    names = [f"synthetic/{i:07d}.png" for i in range(n)]
+    path = os.path.join(tmpdir, f"index_w{world}.pt")
+    t0 = time.perf_counter()
+    rows = rebuild_index(model, ClipProcessor(cfg), [""] * n, names, path, batch_size=512, from_images=True,
+                         images=src, exchange=exchange)
+    dt = time.perf_counter() - t0
+    res = {"world": world, "rank": rank, "seconds": round(dt, 2), "rows_device": str(rows.device),
+           "rows_shape": list(rows.shape), "rows_sha": fold_sha256(rows)}
+    if world > 1:
+        shas = [None] * world
+        dist.all_gather_object(shas, res["rows_sha"])
+        res["rank_shas"] = shas
+    if rank == 0:
+        obj = torch.load(path, map_location="cpu", weights_only=True)
+        emb = obj["embeddings"]
+        res.update({"file_rows": int(emb.shape[0]), "file_dtype": str(emb.dtype), "file_sha": fold_sha256(emb),
+                    "paths_ok": len(obj["image_paths"]) == n and all(obj["image_paths"][i] == names[i]
+                                                                     for i in (0, 1, 12345, n // 2, n - 1)),
+                    "texts_ok": len(obj["texts"]) == n,
+                    "unit_rows": float((emb.double().norm(dim=1) - 1).abs().max())})
+        del obj, emb
+        os.remove(path)
+        json.dump(res, open(out_path, "w"))
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+    model.close()
+
+
+if __name__ == "__main__":
+    main(sys.argv[1], sys.argv[2], int(sys.argv[3]), sys.argv[4])

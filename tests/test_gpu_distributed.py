@@ -41,6 +41,53 @@ def test_sharded_build_and_search_world2(tmp_path):
     assert r["big_file_rows"] == 65_536
 
 
+N_1M = 1_000_000
+
+
+@pytest.fixture(scope="module")
+def index_1m(tmp_path_factory):
+    """configs[2] at its stated size (rebuild_index over 1 M device-generated images, fp16 all_gather
+    exchange), run once per world size {1, 2} by tests/dist_index_worker.py; results by world."""
+    d = tmp_path_factory.mktemp("index_1m")
+    return {"dir": d, "res": {}}
+
+
+def _run_index_1m(index_1m, world):
+    out = index_1m["dir"] / f"w{world}.json"
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
+           "--master-addr=127.0.0.1", f"--master-port={_port()}", os.path.join(REPO, "tests", "dist_index_worker.py"),
+           str(out), str(index_1m["dir"]), str(N_1M), "fp16"]
+    p = subprocess.run(cmd, env=dict(os.environ, MASTER_ADDR="127.0.0.1"), capture_output=True, text=True,
+                       timeout=170)
+    assert p.returncode == 0, p.stderr[-3000:]
+    r = json.loads(out.read_text())
+    index_1m["res"][world] = r
+    return r
+
+
+def test_index_build_1m_world1(index_1m):
+    """BASELINE configs[2] at 1 M images on one rank: the returned rows are the file's, 1 M unit rows
+    with every image path in place (scripts/rebuild_index.py:64-96)."""
+    r = _run_index_1m(index_1m, 1)
+    assert r["file_rows"] == N_1M and r["rows_shape"] == [N_1M, 512]
+    assert r["rows_device"] == "cpu"          # the writing process returns host rows
+    assert r["file_sha"] == r["rows_sha"] and r["file_dtype"] == "torch.float32"
+    assert r["paths_ok"] and r["texts_ok"] and r["unit_rows"] < 1e-6
+
+
+def test_index_build_1m_world2(index_1m):
+    """The same build sharded over 2 ranks (gloo on one GPU; RCCL on the 8-GPU node): every rank
+    gathers the same 1 M rows (fp16 exchange), rank 0 keeps them on the host, rank 1 on its
+    device, and the index is bit-identical to the world-1 build (fold checksum)."""
+    if 1 not in index_1m["res"]:
+        pytest.skip("needs the world-1 result (run the module)")
+    r = _run_index_1m(index_1m, 2)
+    r1 = index_1m["res"][1]
+    assert r["file_rows"] == N_1M and r["paths_ok"] and r["texts_ok"]
+    assert r["rank_shas"] == [r1["rows_sha"]] * 2
+    assert r["file_sha"] == r1["file_sha"] == r1["rows_sha"]
+
+
 def test_rccl_collectives(tmp_path):
     """Every collective of the product and bench.py through an RCCL ("nccl") process group on the
     box's GPU(s): one rank per visible GPU (one on a 1-GPU box)."""

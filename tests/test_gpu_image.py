@@ -95,6 +95,12 @@ def test_resize_crop_c_abi_host_buffers_and_errors():
     with pytest.raises(ValueError):
         _capi.check(L.clm_resize_crop(0, flat.ctypes.data, offs.ctypes.data_as(P64), bad.ctypes.data_as(P32), 3,
                                       224, out.ctypes.data, None))
+    # a 1 x 10^7 strip: its long side would resize to 2.24e9 pixels (past int) -- refused before any
+    # byte is read, as PIL refuses it
+    strip = np.array([1, 10_000_000], np.int32)
+    with pytest.raises(ValueError):
+        _capi.check(L.clm_resize_crop(0, flat.ctypes.data, offs.ctypes.data_as(P64), strip.ctypes.data_as(P32), 1,
+                                      224, out.ctypes.data, None))
 
 
 def _load(tmp_path, max_batch=8):

@@ -539,6 +539,29 @@ def test_shard_roundtrip_bit_identical_to_pt_reload(tmp_path):
     assert torch.equal(ia, ib) and torch.equal(sa, sb) and ia[:, 0].tolist() == list(range(12000, 12004))
 
 
+def test_empty_index_shard_roundtrip(tmp_path):
+    """An index saved while empty (a FinderIndex before its first report) reloads as an empty index
+    that accepts appends and searches them (no data sections to map at n = 0)."""
+    from clip_lora_match_amd.search import TextSearchIndex
+    pt = tmp_path / "empty.pt"
+    torch.save({"embeddings": torch.empty((0, 512)), "image_paths": [], "texts": []}, pt)
+    a = TextSearchIndex(pt)
+    shard = tmp_path / "empty.clmidx"
+    a.save_shard(shard)
+    b = TextSearchIndex.load_shard(shard)
+    assert b.num_items == 0 and b.dim == 512 and b.embeddings.shape == (0, 512)
+    rows = torch.from_numpy(syn.gaussian_rows(6, 512, 75, fp16=False))
+    b.append(rows, [f"p{i}" for i in range(6)], [""] * 6)
+    s, i = b.search_batch(rows[:3], 2)
+    assert i[:, 0].tolist() == [0, 1, 2]
+    idx = CosineIndex(64)
+    idx.save_shard(tmp_path / "empty64.clmidx")
+    re_, hdr = CosineIndex.load_shard(tmp_path / "empty64.clmidx")
+    assert hdr["n"] == 0 and len(re_) == 0
+    idx.close()
+    re_.close()
+
+
 def test_fp16_shard_roundtrip_and_bad_files(tmp_path):
     """An fp16 CosineIndex (no fp32 copy, the configs[4] layout) in small chunks; a file that is
     not a shard raises ValueError, a missing one FileNotFoundError."""
