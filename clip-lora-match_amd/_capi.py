@@ -18,6 +18,7 @@ CLM_OK, CLM_E_ARG, CLM_E_OOM, CLM_E_HIP, CLM_E_STATE, CLM_E_MISSING = 0, -1, -2,
 CLM_F32, CLM_F16, CLM_BF16, CLM_U8, CLM_I32, CLM_I64 = 0, 1, 2, 3, 4, 5
 CLM_PIX_U8_HWC, CLM_PIX_F32_CHW = 0, 1
 CLM_LORA_MERGED, CLM_LORA_UNMERGED = 0, 1
+CLM_COMPUTE_MIXED = 0x12   # bf16 vision tower, fp16 text tower (clm.h)
 CLM_PAIR_GRAPH = 1
 CLM_PAIR_SPLIT_SHIFT = 8
 

@@ -166,7 +166,10 @@ struct clm_ctx {
   struct Rec { int cat; double work; size_t e0, e1; };
   std::vector<Rec> recs;
 
-  bool bf16() const { return desc.compute_dtype == CLM_BF16; }
+  // operand type of a tower's GEMMs / attention (CLM_COMPUTE_MIXED: bf16 vision, fp16 text)
+  bool bf16(bool vision) const {
+    return desc.compute_dtype == CLM_BF16 || (vision && desc.compute_dtype == CLM_COMPUTE_MIXED);
+  }
 
   template <typename T>
   int dalloc(T** p, size_t count) {
@@ -246,9 +249,9 @@ int upload_f32(clm_ctx* c, const std::vector<float>& v, float** dst) {
   return CLM_OK;
 }
 
-int upload_16(clm_ctx* c, const std::vector<float>& v, u16** dst) {
+int upload_16(clm_ctx* c, const std::vector<float>& v, u16** dst, bool bf) {
   std::vector<u16> h(v.size());
-  if (c->bf16())
+  if (bf)
     for (size_t i = 0; i < v.size(); ++i) h[i] = host_f32_to_bf16(v[i]);
   else
     for (size_t i = 0; i < v.size(); ++i) h[i] = host_f32_to_f16(v[i]);
@@ -370,25 +373,25 @@ int build_tower(clm_ctx* c, Tower& T, bool vision) {
                                    {p + ".self_attn.k_proj", T.d, T.d, (tg & CLM_LORA_K) != 0},
                                    {p + ".self_attn.v_proj", T.d, T.d, (tg & CLM_LORA_V) != 0}};
     if ((r = build_fused(c, qkv, true, W, b, K, A, rext))) return r;
-    if ((r = upload_16(c, W, &Lw.w_qkv)) || (r = upload_f32(c, b, &Lw.b_qkv))) return r;
+    if ((r = upload_16(c, W, &Lw.w_qkv, c->bf16(vision))) || (r = upload_f32(c, b, &Lw.b_qkv))) return r;
     Lw.k_qkv = K; Lw.r_qkv = rext;
     if (unmerged && rext && (r = upload_f32(c, A, &Lw.a_qkv))) return r;
 
     std::vector<LinearSpec> outp = {{p + ".self_attn.out_proj", T.d, T.d, (tg & CLM_LORA_OUT) != 0}};
     if ((r = build_fused(c, outp, false, W, b, K, A, rext))) return r;
-    if ((r = upload_16(c, W, &Lw.w_out)) || (r = upload_f32(c, b, &Lw.b_out))) return r;
+    if ((r = upload_16(c, W, &Lw.w_out, c->bf16(vision))) || (r = upload_f32(c, b, &Lw.b_out))) return r;
     Lw.k_out = K; Lw.r_out = rext;
     if (unmerged && rext && (r = upload_f32(c, A, &Lw.a_out))) return r;
 
     std::vector<LinearSpec> fc1 = {{p + ".mlp.fc1", T.d, T.mlp, (tg & CLM_LORA_FC1) != 0}};
     if ((r = build_fused(c, fc1, false, W, b, K, A, rext))) return r;
-    if ((r = upload_16(c, W, &Lw.w_fc1)) || (r = upload_f32(c, b, &Lw.b_fc1))) return r;
+    if ((r = upload_16(c, W, &Lw.w_fc1, c->bf16(vision))) || (r = upload_f32(c, b, &Lw.b_fc1))) return r;
     Lw.k_fc1 = K; Lw.r_fc1 = rext;
     if (unmerged && rext && (r = upload_f32(c, A, &Lw.a_fc1))) return r;
 
     std::vector<LinearSpec> fc2 = {{p + ".mlp.fc2", T.mlp, T.d, (tg & CLM_LORA_FC2) != 0}};
     if ((r = build_fused(c, fc2, false, W, b, K, A, rext))) return r;
-    if ((r = upload_16(c, W, &Lw.w_fc2)) || (r = upload_f32(c, b, &Lw.b_fc2))) return r;
+    if ((r = upload_16(c, W, &Lw.w_fc2, c->bf16(vision))) || (r = upload_f32(c, b, &Lw.b_fc2))) return r;
     Lw.k_fc2 = K; Lw.r_fc2 = rext;
     if (unmerged && rext && (r = upload_f32(c, A, &Lw.a_fc2))) return r;
   }
@@ -417,7 +420,7 @@ int build_tower(clm_ctx* c, Tower& T, bool vision) {
     if ((r = need(c, pre + ".embeddings.patch_embedding.weight", (int64_t)T.d * kreal, &pw))) return r;
     std::vector<float> wp((size_t)T.d * T.kp, 0.f);
     for (int o = 0; o < T.d; ++o) std::memcpy(&wp[(size_t)o * T.kp], &pw->data[(size_t)o * kreal], kreal * 4);
-    if ((r = upload_16(c, wp, &T.patch_w))) return r;
+    if ((r = upload_16(c, wp, &T.patch_w, c->bf16(true)))) return r;
     // CLIPImageProcessor rescale (float64 multiply -> float32) then (x - mean) / std in float32
     std::vector<float> lut((size_t)d.channels * 256);
     for (int ch = 0; ch < d.channels; ++ch)
@@ -559,7 +562,7 @@ bool fused_attention(int T, int H, int d, int K) {
 // removed: profiles/r02_v2_ln_fold_ab.txt.)
 int run_layers(clm_ctx* c, Tower& T, int B, int S, bool causal, const int32_t* ids, bool* pooled_rows,
                hipStream_t st, bool vl = false) {
-  const bool bf = c->bf16();
+  const bool bf = c->bf16(T.vision);
   const bool prune = prune_last_layer();
   *pooled_rows = false;
   // varlen (packed live text rows): the row-wise kernels read the live row count from
@@ -684,7 +687,7 @@ Tower ws_view(const Tower& T0, int b0, int rows, int patches, int proj_dim) {
 int encode_image_chunk(clm_ctx* c, Tower& T, const void* pix, int layout, int B, void* out, int out_dtype,
                        int normalize, hipStream_t st) {
   const clm_model_desc& d = c->desc;
-  const bool bf = c->bf16();
+  const bool bf = c->bf16(T.vision);
   const int G = d.image_size / d.patch, Tn = G * G + 1;
   { PROF(CLM_PROF_OTHER, (double)B * G * G * T.kp * 2.0 + (double)B * d.image_size * d.image_size * d.channels);
     KCHK(patchify(bf, pix, layout, B, d.image_size, d.patch, d.channels, T.lut, T.P, T.kp, st)); }
@@ -708,7 +711,7 @@ int encode_image_chunk(clm_ctx* c, Tower& T, const void* pix, int layout, int B,
 int encode_text_chunk(clm_ctx* c, Tower& T, const int32_t* ids_dev, int B, int L, void* out, int out_dtype,
                       int normalize, hipStream_t st) {
   const clm_model_desc& d = c->desc;
-  const bool bf = c->bf16();
+  const bool bf = c->bf16(T.vision);
   LnArgs a{};
   a.mode = 1; a.ids = ids_dev; a.tok = T.tok; a.pos = T.tpos; a.L = L;
   a.hf = T.h; a.ldh = T.d; a.g1 = T.layers[0].ln1_g; a.b1 = T.layers[0].ln1_b;
@@ -837,8 +840,8 @@ int clm_ctx_create(int hip_device, const clm_model_desc* desc, clm_ctx** out) {
     return fail(CLM_E_HIP, "no HIP device available");
   }
   if (hip_device < 0 || hip_device >= ndev) return fail(CLM_E_ARG, "bad device index");
-  if (desc->compute_dtype != CLM_BF16 && desc->compute_dtype != CLM_F16)
-    return fail(CLM_E_ARG, "compute_dtype must be CLM_BF16 or CLM_F16");
+  if (desc->compute_dtype != CLM_BF16 && desc->compute_dtype != CLM_F16 && desc->compute_dtype != CLM_COMPUTE_MIXED)
+    return fail(CLM_E_ARG, "compute_dtype must be CLM_BF16, CLM_F16 or CLM_COMPUTE_MIXED");
   if (desc->max_batch <= 0 || desc->patch <= 0 || desc->image_size % desc->patch)
     return fail(CLM_E_ARG, "bad max_batch / patch / image_size");
   if (desc->max_pos > 77 * 4 || desc->proj_dim > 1024) return fail(CLM_E_ARG, "bad max_pos / proj_dim");

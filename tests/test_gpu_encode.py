@@ -8,6 +8,10 @@ Tolerances (written here, derived in DESIGN.md §Numerics):
   * bf16 operands (BASELINE config 1's wording): 3 fewer mantissa bits in every GEMM
     operand; measured max score error 1.7e-3 on the 64 + 64 parity set (over the 1e-3 bar,
     which is why fp16 is the headline), bar 2.5e-3, 1 - cos <= 1e-4.
+  * "mixed" (CLM_COMPUTE_MIXED: bf16 operands in the vision tower, fp16 in the text tower): the
+    text tower carries the bf16 error (profiles/r04_v2_bf16_tower_bisect.jsonl), so this bf16
+    assignment meets the 1e-3 score bar (measured 6.0e-4 on the parity set); 1 - cos <= 1e-4
+    (the vision embeddings' bf16 distance, measured 1.2e-5).
 """
 import numpy as np
 import pytest
@@ -20,7 +24,8 @@ from clip_lora_match_amd import synthetic as syn
 from clip_lora_match_amd.engine import ClipLoraModel
 from oracle import clip_ref as R
 
-TOL = {"float16": dict(score=1e-3, cos=1e-5), "bfloat16": dict(score=2.5e-3, cos=1e-4)}
+TOL = {"float16": dict(score=1e-3, cos=1e-5), "bfloat16": dict(score=2.5e-3, cos=1e-4),
+       "mixed": dict(score=1e-3, cos=1e-4)}
 
 pytestmark = pytest.mark.gpu
 
@@ -44,7 +49,7 @@ def _check(gi, gt, ri, rt, dtype):
         assert err <= tol["score"], f"score error {err:.3e} > {tol['score']}"
 
 
-@pytest.mark.parametrize("dtype", ["float16", "bfloat16"])
+@pytest.mark.parametrize("dtype", ["float16", "bfloat16", "mixed"])
 @pytest.mark.parametrize("mode", ["merged", "unmerged"])
 def test_tiny_vs_oracle(dtype, mode):
     m, cfg, sd, lora = _model("tiny", dtype, mode)
@@ -57,7 +62,7 @@ def test_tiny_vs_oracle(dtype, mode):
     _check(gi, gt, ri, rt, dtype)
 
 
-@pytest.mark.parametrize("dtype", ["float16", "bfloat16"])
+@pytest.mark.parametrize("dtype", ["float16", "bfloat16", "mixed"])
 def test_b32_lora_golden(dtype):
     g = golden("enc_b32_lora.npz")
     m, cfg, sd, lora = _model("ViT-B/32", dtype)
@@ -69,7 +74,7 @@ def test_b32_lora_golden(dtype):
     assert np.max(np.abs(g["emb_txt"] - g["emb_txt_base"])) > 10 * TOL[dtype]["score"]
 
 
-@pytest.mark.parametrize("dtype", ["float16", "bfloat16"])
+@pytest.mark.parametrize("dtype", ["float16", "bfloat16", "mixed"])
 def test_b32_lora_parity_set_64(dtype):
     """the 64 images + 64 captions bench.py's `parity` object scores (whole 128 x 128 score
     matrix); prints the measured errors"""
@@ -100,10 +105,11 @@ def test_b32_unmerged_matches_merged():
 # the square root of the number of rounded GEMM inputs along the path) and a rank-16 adapter on
 # every Linear, so the B/32 bf16 bars scale by ~sqrt(2): scores 6e-3, 1 - cos 2e-4 (measured on
 # MI355X: see DESIGN.md §Numerics). fp16 keeps the north_star 1e-3 bar.
-TOL_L14 = {"float16": dict(score=1e-3, cos=1e-5), "bfloat16": dict(score=6e-3, cos=2e-4)}
+TOL_L14 = {"float16": dict(score=1e-3, cos=1e-5), "bfloat16": dict(score=6e-3, cos=2e-4),
+           "mixed": dict(score=1e-3, cos=2e-4)}
 
 
-@pytest.mark.parametrize("dtype", ["float16", "bfloat16"])
+@pytest.mark.parametrize("dtype", ["float16", "bfloat16", "mixed"])
 def test_l14_lora_golden(dtype):
     g = golden("enc_l14_lora.npz")
     m, cfg, _, _ = _model("ViT-L/14@336", dtype, max_batch=8)
