@@ -64,6 +64,12 @@ def _worker(rank, world, port, n, dim, nq, k, q):
         # index build: every rank "encodes" its shard (identity here), one all_gather
         got = build_index_sharded(lambda s, e: torch.from_numpy(full[s:e] * 2.0), n, batch=7)
         assert torch.equal(got, torch.from_numpy(full * 2.0))
+        # the fp16 exchange form (index_build exchange="fp16"): the rows cross the links as fp16 and
+        # are restored after the gather -- equal to the same round trip done without ranks
+        got16 = build_index_sharded(lambda s, e: torch.from_numpy(full[s:e]), n, batch=5,
+                                    exchange=lambda r: r.to(torch.float16), restore=lambda r: r.float() * 3.0)
+        assert got16.dtype == torch.float32
+        assert torch.equal(got16, torch.from_numpy(full).to(torch.float16).float() * 3.0)
         # sharded search
         idx = ShardedIndex(dim, n, local_factory=_OracleShard)
         idx.append_shard(torch.from_numpy(full[idx.start:idx.stop]))
