@@ -1609,6 +1609,7 @@ static int search_bounded(clm_index* x, bool sampled, int64_t S, const u16* q16,
     gf.theta = th + q0; gf.theta_ld = 1;
     gf.cnt = cnt; gf.cand_s = cs; gf.cand_i = ci; gf.cap = CAND_CAP; gf.base = x->offset;
     gf.m_fastest = 1;
+    gf.debug = g_gemm_debug & 3;   // diagnostics only ($CLM_GEMM_DEBUG): main loop alone / stores dropped
     KCHK(gemm(false, EPI_FILTER, gf, st));
     KCHK(rescore_select(cs, ci, cnt, CAND_CAP, q32 + q0 * dim, qn + q0, dim, xrows, !x->rows32, x->offset,
                         RESCORE_MARGIN, nb, k, osc + q0 * k, oix + q0 * k, st));
