@@ -220,6 +220,8 @@ struct clm_index {
   void* ws4 = nullptr; size_t ws4_bytes = 0;
   // strided row sample for the threshold pass, rebuilt when n changes
   u16* samp = nullptr; float* samp_inv = nullptr; int64_t samp_S = 0, samp_n = -1, samp_cap = 0;
+  // order keys {min, max} of inv[0, n) for the filter GEMM's skip test, rebuilt with the sample
+  unsigned* inv_keys = nullptr; int64_t inv_keys_n = -1;
   // queries served by: [0] sampled bounded search, [1] the full exact scan, [2] overflow re-runs,
   // [3] bounded search with the chunked fp16 scan as step 1
   int64_t search_stats[4] = {0, 0, 0, 0};
@@ -1152,7 +1154,7 @@ int clm_index_destroy(clm_index* x) {
   DeviceGuard g(x->dev);
   (void)hipDeviceSynchronize();
   for (void* p : {(void*)x->rows, (void*)x->inv, (void*)x->rows32, x->ws, x->ws2, x->ws3, x->ws4, (void*)x->samp,
-                  (void*)x->samp_inv})
+                  (void*)x->samp_inv, (void*)x->inv_keys})
     if (p) (void)hipFree(p);
   delete x;
   return CLM_OK;
@@ -1202,6 +1204,7 @@ int clm_index_append(clm_index* x, const void* rows, int dtype, int64_t n, void*
   int r = index_grow(x, x->n + n);
   if (r) return r;
   x->samp_n = -1;   // the threshold sample is rebuilt from the new row set
+  x->inv_keys_n = -1;
   if (dtype == CLM_F32 && !x->rows32) {
     // first fp32 rows: keep an fp32 copy from now on; the rows so far were fp16 as given
     if (hipMalloc(&x->rows32, (size_t)x->cap * x->dim * sizeof(float)) != hipSuccess) {
@@ -1278,6 +1281,7 @@ int clm_index_import(clm_index* x, const uint16_t* rows16, const float* inv, con
   int r = index_grow(x, x->n + n);
   if (r) return r;
   x->samp_n = -1;
+  x->inv_keys_n = -1;
   const size_t cnt = (size_t)n * x->dim;
   if (rows32 && !x->rows32) {   // as clm_index_append: the first fp32 rows start the fp32 copy
     if (hipMalloc(&x->rows32, (size_t)x->cap * x->dim * sizeof(float)) != hipSuccess) {
@@ -1306,6 +1310,7 @@ int clm_index_reset(clm_index* x) {
   if (!x) return fail(CLM_E_ARG, "null index");
   x->n = 0;
   x->samp_n = -1;   // never reuse a sample of the previous rows
+  x->inv_keys_n = -1;
   return CLM_OK;
 }
 
@@ -1434,6 +1439,26 @@ static int search_scan(clm_index* x, bool exact, const u16* q16, const float* qi
   return CLM_OK;
 }
 
+// The filter GEMM's cscale bounds (GemmArgs::cbound) for the current rows, computed once per row set
+// on the stream. Null (no skip test) when $CLM_FILTER_SKIP=0 (A/B) or the 8 bytes cannot be had.
+static const unsigned* inv_keys_of(clm_index* x, hipStream_t st) {
+  static const bool on = !getenv("CLM_FILTER_SKIP") || atoi(getenv("CLM_FILTER_SKIP")) != 0;
+  if (!on) return nullptr;
+  if (!x->inv_keys && hipMalloc(&x->inv_keys, 2 * sizeof(unsigned)) != hipSuccess) {
+    (void)hipGetLastError();
+    x->inv_keys = nullptr;
+    return nullptr;
+  }
+  if (x->inv_keys_n != x->n) {
+    if (value_bounds(x->inv, x->n, x->inv_keys, st) != hipSuccess) {
+      (void)hipGetLastError();
+      return nullptr;
+    }
+    x->inv_keys_n = x->n;
+  }
+  return x->inv_keys;
+}
+
 // Overflowed queries, wide path: their fp16 rows, inverse norms, fp32 rows, norms and filter
 // thresholds are gathered, the EPI_FILTER GEMM streams the index once more for just them with a
 // capacity of cap[j] (the first pass's count plus headroom), and rescore_wide + topk_merge pick the
@@ -1482,6 +1507,7 @@ static int overflow_wide(clm_index* x, const std::vector<int64_t>& qs, const std
     gf.theta = (const float*)(w + p_th); gf.theta_ld = 1;
     gf.cnt = cnt; gf.cand_s = (float*)(w + p_cs); gf.cand_i = (int64_t*)(w + p_ci); gf.cap = (int)cap_max;
     gf.base = x->offset; gf.m_fastest = 1;
+    gf.cbound = inv_keys_of(x, st);
     if ((e = gemm(false, EPI_FILTER, gf, st)) != hipSuccess) break;
     if ((e = rescore_wide((const int64_t*)(w + p_ci), cnt, cap_max, (const float*)(w + p_q32),
                           (const double*)(w + p_qn), dim, xrows, !x->rows32, x->offset, ng, k, (float*)(w + p_ps),
@@ -1609,6 +1635,7 @@ static int search_bounded(clm_index* x, bool sampled, int64_t S, const u16* q16,
     gf.theta = th + q0; gf.theta_ld = 1;
     gf.cnt = cnt; gf.cand_s = cs; gf.cand_i = ci; gf.cap = CAND_CAP; gf.base = x->offset;
     gf.m_fastest = 1;
+    gf.cbound = inv_keys_of(x, st);
     gf.debug = g_gemm_debug & 3;   // diagnostics only ($CLM_GEMM_DEBUG): main loop alone / stores dropped
     KCHK(gemm(false, EPI_FILTER, gf, st));
     KCHK(rescore_select(cs, ci, cnt, CAND_CAP, q32 + q0 * dim, qn + q0, dim, xrows, !x->rows32, x->offset,

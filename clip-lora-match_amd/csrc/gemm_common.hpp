@@ -148,7 +148,7 @@ __device__ __forceinline__ void epilogue(const GemmArgs& g, const f32x4 (&acc)[B
   float4 cv[C::TN];
 #pragma unroll
   for (int nb = 0; nb < C::TN; ++nb) {
-    if constexpr (!HOIST) break;
+    if constexpr (!HOIST || EPI == EPI_FILTER) break;   // FILTER: loaded after its skip test
     const int n = wcol + nb * 16;
     if constexpr (EPI == EPI_SCORE || EPI == EPI_FILTER)
       cv[nb] = (g.cscale && n < g.N) ? *(const float4*)(g.cscale + n) : make_float4(1.f, 1.f, 1.f, 1.f);
@@ -300,6 +300,56 @@ __device__ __forceinline__ void epilogue(const GemmArgs& g, const f32x4 (&acc)[B
         }
       }
     } else {
+      // Skip test: with cmin = min cscale >= 0 and cmax = max cscale finite, every score of a
+      // 16 x 16 block, (acc * rs) * c, is at most (mx * rs) * (mx >= 0 ? cmax : cmin), mx = the
+      // block's largest accumulator on the lane (fp32 multiplication is monotonic; same operation
+      // order as the scores), so a row block / block that no lane of the wave can append from is
+      // skipped whole, before its cscale loads. Out-of-range columns (clamped operand rows) only
+      // raise mx. The appended (score, row) set is exactly the unskipped path's.
+      if (g.cbound) {
+        const float cmin = key_float(g.cbound[0]), cmax = key_float(g.cbound[1]);
+        const bool cok = cmin >= 0.f && cmax <= 3.4028235e38f;   // NaN fails both
+#pragma unroll
+        for (int mb = 0; mb < C::TM; ++mb) {
+          const int m = wrow + mb * 16;
+          const bool live = m < g.M;
+          const bool rok = cok && rs[mb] >= 0.f && rs[mb] <= 3.4028235e38f && th[mb] >= -3.4028235e38f;
+          float bmx[C::TN];
+          float mx = -3.4028235e38f;
+#pragma unroll
+          for (int nb = 0; nb < C::TN; ++nb) {
+            bmx[nb] = fmaxf(fmaxf(acc[mb][nb][0], acc[mb][nb][1]), fmaxf(acc[mb][nb][2], acc[mb][nb][3]));
+            mx = fmaxf(mx, bmx[nb]);
+          }
+          auto reach = [&](float v) { return live && (!rok || (v * rs[mb]) * (v >= 0.f ? cmax : cmin) >= th[mb]); };
+          if (!__any(reach(mx))) continue;
+#pragma unroll
+          for (int nb = 0; nb < C::TN; ++nb) {
+            if (!__any(reach(bmx[nb]))) continue;
+            const int n = wcol + nb * 16;
+            if (!live || n >= g.N) continue;
+            const float4 c = g.cscale ? *(const float4*)(g.cscale + n) : make_float4(1.f, 1.f, 1.f, 1.f);
+            const float sc[4] = {acc[mb][nb][0] * rs[mb] * c.x, acc[mb][nb][1] * rs[mb] * c.y,
+                                 acc[mb][nb][2] * rs[mb] * c.z, acc[mb][nb][3] * rs[mb] * c.w};
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              if (sc[j] >= th[mb]) {
+                const int slot = atomicAdd(g.cnt + m, 1);
+                if (slot < g.cap) {
+                  g.cand_s[(int64_t)m * g.cap + slot] = sc[j];
+                  g.cand_i[(int64_t)m * g.cap + slot] = g.base + n + j;
+                }
+              }
+            }
+          }
+        }
+        return;
+      }
+#pragma unroll
+      for (int nb = 0; nb < C::TN; ++nb) {
+        const int n = wcol + nb * 16;
+        cv[nb] = (g.cscale && n < g.N) ? *(const float4*)(g.cscale + n) : make_float4(1.f, 1.f, 1.f, 1.f);
+      }
 #pragma unroll
       for (int mb = 0; mb < C::TM; ++mb) {
         const int m = wrow + mb * 16;

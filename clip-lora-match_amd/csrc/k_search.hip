@@ -481,6 +481,32 @@ hipError_t filter_thresholds(const float* ts, int64_t ld, int64_t nq, int k, flo
   return hipGetLastError();
 }
 
+__global__ __launch_bounds__(256) void value_bounds_kernel(const float* v, int64_t n, unsigned* keys) {
+  unsigned lo = 0xFFFFFFFFu, hi = 0u;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    const unsigned k = float_key(v[i]);
+    lo = min(lo, k);
+    hi = max(hi, k);
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    lo = min(lo, (unsigned)__shfl_xor((int)lo, o));
+    hi = max(hi, (unsigned)__shfl_xor((int)hi, o));
+  }
+  if ((threadIdx.x & 63) == 0) {
+    atomicMin(keys, lo);
+    atomicMax(keys + 1, hi);
+  }
+}
+
+hipError_t value_bounds(const float* v, int64_t n, unsigned* keys, hipStream_t s) {
+  hipError_t e = hipMemsetD32Async((hipDeviceptr_t)keys, 0xFFFFFFFFu, 1, s);
+  if (e == hipSuccess) e = hipMemsetD32Async((hipDeviceptr_t)(keys + 1), 0u, 1, s);
+  if (e != hipSuccess || n <= 0) return e;
+  const int blocks = (int)std::min<int64_t>((n + 255) / 256, 2048);
+  value_bounds_kernel<<<blocks, 256, 0, s>>>(v, n, keys);
+  return hipGetLastError();
+}
+
 hipError_t f16_to_f32_rows(const u16* src, int64_t n, int dim, float* dst, hipStream_t s) {
   const int64_t total = n * dim;
   if (total <= 0) return hipSuccess;

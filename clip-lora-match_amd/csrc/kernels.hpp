@@ -29,6 +29,9 @@ struct GemmArgs {
   const float* rscale; const float* cscale;
   // EPI_FILTER
   const float* theta; int64_t theta_ld; int* cnt; float* cand_s; int64_t* cand_i; int cap; int64_t base;
+  // optional: order keys {min, max} of cscale[0, N) (value_bounds); lets a wave whose largest
+  // accumulator cannot reach any of its rows' thresholds skip the per-element filter
+  const unsigned* cbound;
   int m_fastest;   // tile order: 1 = consecutive workgroups walk M (share one W tile)
   // split-K (gemm_kernel configs only, EPI_SCORE as the fp32 partial store): ksplit > 1 cuts K
   // into ksplit equal slices; slice s of every tile writes out + s * split_stride
@@ -196,5 +199,15 @@ hipError_t gather_rows(const void* src, int64_t src_stride, const int64_t* idx, 
                        void* dst, int64_t dst_stride, bool scatter, hipStream_t s);
 // th[q] = ts[q * ld + k - 1] - margin
 hipError_t filter_thresholds(const float* ts, int64_t ld, int64_t nq, int k, float margin, float* th, hipStream_t s);
+// keys[0] / keys[1] = order key (float_key) of min / max over v[0, n); a NaN anywhere makes the
+// decoded min or max NaN. keys: 2 device u32
+hipError_t value_bounds(const float* v, int64_t n, unsigned* keys, hipStream_t s);
+__host__ __device__ inline unsigned float_key(float f) {
+  const unsigned b = __builtin_bit_cast(unsigned, f);
+  return (b & 0x80000000u) ? ~b : (b | 0x80000000u);
+}
+__host__ __device__ inline float key_float(unsigned k) {
+  return __builtin_bit_cast(float, (k & 0x80000000u) ? (k & 0x7FFFFFFFu) : ~k);
+}
 
 }  // namespace clm

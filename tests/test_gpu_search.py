@@ -344,6 +344,38 @@ def test_overflow_wide_and_exact_paths(monkeypatch, k):
     idx.close()
 
 
+@pytest.mark.parametrize("case", ["negative_topk", "wide_norms", "zero_row"])
+def test_filter_skip_test_edge_cases(monkeypatch, case):
+    """The filter GEMM skips a wave when (max acc * rscale) * (max or min cscale) is below every
+    row's threshold (GemmArgs::cbound). Cases that exercise each side of that bound agree bit for
+    bit with the full exact scan: all top-k scores negative (thresholds < 0: the min-cscale side),
+    fp16 rows with norms over 4 decades (cscale spread 1e4), and a zero row (inverse norm inf:
+    the bound is off and every element is tested)."""
+    monkeypatch.setenv("CLM_SEARCH_BOUNDED", "1")
+    n, dim, k = 300_000, 128, 10
+    g = torch.Generator(device="cuda").manual_seed(21)
+    rows = torch.randn((n, dim), generator=g, device="cuda")
+    q = torch.randn((24, dim), generator=g, device="cuda")
+    if case == "negative_topk":
+        rows = rows.abs() + 0.05           # every row in the positive orthant
+        q = -(q.abs() + 0.05)              # every query in the negative one: all cosines < 0
+    elif case == "wide_norms":
+        rows = rows * torch.exp(torch.empty((n, 1), device="cuda").uniform_(-4.6, 4.6, generator=g))
+    else:
+        rows[12345] = 0
+    idx = CosineIndex(dim, capacity=n)
+    idx.append(rows.half())
+    s, i = idx.search(q.half(), k)
+    assert idx.stats()["filtered"] + idx.stats()["overflow"] >= 24
+    if case == "negative_topk":
+        assert torch.all(s < 0)
+    monkeypatch.delenv("CLM_SEARCH_BOUNDED")
+    monkeypatch.setenv("CLM_SEARCH_FULL", "1")
+    s_ref, i_ref = idx.search(q.half(), k)
+    assert torch.equal(i, i_ref) and torch.equal(s, s_ref)
+    idx.close()
+
+
 # ---- query fusion (seeker_service.py:84-186) ------------------------------------------------
 def _unit_rows(n, d, seed):
     x = np.random.default_rng(seed).standard_normal((n, d)).astype(np.float32)

@@ -1,6 +1,6 @@
 """PP GEMM probe: per encoder shape, check the PP configs (12-16, k_gemm3.hip) bit for bit against
 the picked gemm_kernel / G2 config on the same random fp16 operands and epilogue, then time full /
-main-loop-only (debug bit 1) of every config, interleaved in ONE process (median of rounds).
+main-loop-only (debug bit 1) / epilogue without its stores (debug bit 2) of every config, interleaved in ONE process (median of rounds).
 usage: python tools/pp_probe.py [cfg,cfg,...] [shape,shape,...] -> one JSON line per (shape, variant)"""
 import json
 import os
@@ -83,6 +83,7 @@ for name in only:
         bufs[cfg] = fresh()
         variants[f"c{cfg}_full"] = (lambda c: lambda: run(c, bufs[c]))(cfg)
         variants[f"c{cfg}_noepi"] = (lambda c: lambda: run(c, bufs[c], 1))(cfg)
+        variants[f"c{cfg}_nostore"] = (lambda c: lambda: run(c, bufs[c], 2))(cfg)
     for fn in variants.values():
         fn()
     torch.cuda.synchronize()
