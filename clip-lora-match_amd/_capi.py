@@ -84,6 +84,8 @@ def lib():
         "clm_cosine_scores": (c_int, [c_int, c_void_p, c_int64, c_void_p, c_int64, c_int, c_void_p, c_void_p]),
         "clm_topk_merge": (c_int, [c_int, c_void_p, c_void_p, c_int64, c_int, c_int, c_int, c_void_p, c_void_p,
                                    c_void_p]),
+        "clm_topk_threshold": (c_int, [c_int, c_void_p, c_int64, c_int64, c_int64, c_int, ctypes.c_float, c_int,
+                                       c_void_p, c_void_p]),
         "clm_l2_normalize": (c_int, [c_int, c_void_p, c_int64, c_int, c_void_p]),
         "clm_fuse_queries": (c_int, [c_int, c_void_p, ctypes.c_float, c_void_p, ctypes.c_float, c_int64, c_int,
                                      c_void_p, c_void_p]),
@@ -120,7 +122,7 @@ EXPORTED = (
     "clm_encode_image", "clm_encode_text", "clm_encode_pair", "clm_index_create", "clm_index_destroy", "clm_index_append",
     "clm_index_size", "clm_index_reset", "clm_index_set_offset", "clm_index_read", "clm_index_search", "clm_index_stats",
     "clm_index_stats2",
-    "clm_cosine_scores", "clm_topk_merge", "clm_l2_normalize", "clm_fuse_queries", "clm_resize_crop", "clm_synth_images", "clm_index_has_f32", "clm_index_export", "clm_index_import",
+    "clm_cosine_scores", "clm_topk_merge", "clm_topk_threshold", "clm_l2_normalize", "clm_fuse_queries", "clm_resize_crop", "clm_synth_images", "clm_index_has_f32", "clm_index_export", "clm_index_import",
     "clm_last_error", "clm_version",
     "clm_model_desc_size", "clm_prof_enable", "clm_prof_read", "clm_gemm", "clm_gemm_num_configs",
     "clm_attention", "clm_layernorm", "clm_debug_set",

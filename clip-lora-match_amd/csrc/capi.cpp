@@ -1556,6 +1556,9 @@ static int overflow_wide(clm_index* x, const std::vector<int64_t>& qs, const std
 //  3. rescore_select: candidates within the margin of their k-th are re-scored exactly against
 //     the caller's rows, sorted (score desc, index asc), top k written.
 //  Lists that overflowed CAND_CAP are redone by the full exact scan.
+// $CLM_KTH_RADIX=1: the sampled thresholds through topk_rows (A/B, tests)
+static const bool g_kth_radix = getenv("CLM_KTH_RADIX") && atoi(getenv("CLM_KTH_RADIX")) != 0;
+
 static int search_bounded(clm_index* x, bool sampled, int64_t S, const u16* q16, const float* qinv,
                           const float* q32, const double* qn, int64_t nq, int k, float* osc, int64_t* oix,
                           hipStream_t st) {
@@ -1622,11 +1625,16 @@ static int search_bounded(clm_index* x, bool sampled, int64_t S, const u16* q16,
       ga.M = (int)nb; ga.N = (int)S; ga.K = dim; ga.out = sc; ga.ldo = S;
       ga.rscale = qinv + q0; ga.cscale = x->samp_inv;
       KCHK(gemm(false, EPI_SCORE, ga, st));
-      KCHK(topk_rows(sc, S, nb, S, k, 0, ts, ti, k, st));
+      if (k <= 8 && !g_kth_radix) {   // one streaming pass for the k-th value alone
+        KCHK(kth_thresholds(sc, S, nb, S, k, RESCORE_MARGIN, th + q0, st));
+      } else {
+        KCHK(topk_rows(sc, S, nb, S, k, 0, ts, ti, k, st));
+        KCHK(filter_thresholds(ts, k, nb, k, RESCORE_MARGIN, th + q0, st));
+      }
     } else {
       if ((r = search_scan(x, false, q16 + q0 * dim, qinv + q0, nullptr, nullptr, nb, k, ts, ti, st))) return r;
+      KCHK(filter_thresholds(ts, k, nb, k, RESCORE_MARGIN, th + q0, st));
     }
-    KCHK(filter_thresholds(ts, k, nb, k, RESCORE_MARGIN, th + q0, st));
     HIPCHK(hipMemsetAsync(cnt, 0, (size_t)nb * 4, st));
     GemmArgs gf{};
     gf.A = q16 + q0 * dim; gf.lda = dim; gf.W = x->rows; gf.ldw = dim;
@@ -1815,6 +1823,30 @@ int clm_cosine_scores(int hip_device, const float* q, int64_t nq, const float* c
   if (e == hipSuccess) e = hipStreamSynchronize(st);
   if (e != hipSuccess) rc = fail(CLM_E_HIP, std::string("cosine_scores: ") + hipGetErrorString(e));
   return rc;
+}
+
+int clm_topk_threshold(int hip_device, const float* scores, int64_t lds, int64_t nq, int64_t C, int k, float margin,
+                       int method, float* th, void* stream) {
+  if (nq < 0 || C < k || lds < C || k < 1 || k > (method == 0 ? 8 : 1024) || (method != 0 && method != 1))
+    return fail(CLM_E_ARG, "bad threshold shape (k <= C <= lds; k <= 8 streaming, <= 1024 radix)");
+  if (nq == 0) return CLM_OK;
+  if (!is_device_ptr(scores) || !is_device_ptr(th)) return fail(CLM_E_ARG, "topk_threshold: device pointers");
+  DeviceGuard g(hip_device);
+  hipStream_t st = (hipStream_t)stream;
+  if (method == 0) {
+    KCHK(kth_thresholds(scores, lds, nq, C, k, margin, th, st));
+    return CLM_OK;
+  }
+  Scratch& scr = scratch_of_current_device();
+  std::lock_guard<std::mutex> lock(scr.mu);
+  const size_t bs = round_up((size_t)nq * k * 4, 256);
+  if (int rg = grow(&scr.p, &scr.bytes, bs + (size_t)nq * k * 8)) return rg;
+  float* ts = (float*)scr.p;
+  int64_t* ti = (int64_t*)((uint8_t*)scr.p + bs);
+  KCHK(topk_rows(scores, lds, nq, C, k, 0, ts, ti, k, st));
+  KCHK(filter_thresholds(ts, k, nq, k, margin, th, st));
+  HIPCHK(hipStreamSynchronize(st));   // the scratch is reused by the next call
+  return CLM_OK;
 }
 
 int clm_topk_merge(int hip_device, const float* scores, const int64_t* idx, int64_t nq, int parts, int k_in, int k,

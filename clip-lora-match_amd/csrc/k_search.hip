@@ -371,6 +371,67 @@ __global__ void theta_kernel(const float* ts, int64_t ld, int64_t nq, int k, flo
   if (i < nq) th[i] = ts[i * ld + k - 1] - margin;
 }
 
+// Threshold of the sampled bounded search: th[row] = (k-th largest of row, by the fkey order, with
+// multiplicity) - margin, the value topk_rows + theta_kernel give, in one streaming pass instead of
+// a radix select's 2-3 passes with LDS-atomic histograms. 256 threads per row: each keeps the 8
+// largest keys of its strided elements in registers (sorted, insertion on the rare key above the
+// 8th), then each wave and finally wave 0 pops the maximum k times (lowest lane first among equal
+// keys, so duplicates count). k <= KTH_MAX.
+constexpr int KTH_MAX = 8;
+__device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
+  for (int o = 32; o > 0; o >>= 1) v = max(v, (uint32_t)__shfl_xor((int)v, o));
+  return v;
+}
+__global__ __launch_bounds__(256) void kth_threshold_kernel(const float* S, int64_t lds, int64_t C, int k, float margin,
+                                                            float* th) {
+  __shared__ uint32_t part[4 * KTH_MAX];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const float* s = S + (int64_t)blockIdx.x * lds;
+  uint32_t t[KTH_MAX];
+#pragma unroll
+  for (int j = 0; j < KTH_MAX; ++j) t[j] = 0u;
+  auto insert = [&](uint32_t x) {
+    if (x <= t[KTH_MAX - 1]) return;
+    t[KTH_MAX - 1] = x;
+#pragma unroll
+    for (int j = KTH_MAX - 1; j > 0; --j)
+      if (t[j] > t[j - 1]) { const uint32_t a = t[j]; t[j] = t[j - 1]; t[j - 1] = a; }
+  };
+  if ((lds & 3) == 0 && ((uintptr_t)S & 15) == 0) {
+    const int64_t C4 = C >> 2;
+    const float4* s4 = (const float4*)s;
+    for (int64_t i = tid; i < C4; i += 256) {
+      const float4 v = s4[i];
+      insert(fkey(v.x)); insert(fkey(v.y)); insert(fkey(v.z)); insert(fkey(v.w));
+    }
+    for (int64_t i = (C4 << 2) + tid; i < C; i += 256) insert(fkey(s[i]));
+  } else {
+    for (int64_t i = tid; i < C; i += 256) insert(fkey(s[i]));
+  }
+  // wave top-k: pop the wave maximum k times
+  uint32_t m = 0;
+  for (int r = 0; r < k; ++r) {
+    m = wave_max_u32(t[0]);
+    const unsigned long long who = __ballot(t[0] == m);
+    if (lane == __ffsll((long long)who) - 1) {
+#pragma unroll
+      for (int j = 0; j < KTH_MAX - 1; ++j) t[j] = t[j + 1];
+      t[KTH_MAX - 1] = 0u;
+    }
+    if (lane == 0) part[wid * KTH_MAX + r] = m;
+  }
+  __syncthreads();
+  if (wid == 0) {
+    uint32_t v = (lane < 4 * KTH_MAX && (lane % KTH_MAX) < k) ? part[lane] : 0u;
+    for (int r = 0; r < k; ++r) {
+      m = wave_max_u32(v);
+      const unsigned long long who = __ballot(v == m);
+      if (lane == __ffsll((long long)who) - 1) v = 0u;
+    }
+    if (lane == 0) th[blockIdx.x] = kfloat(m) - margin;
+  }
+}
+
 __global__ void upcast_f16_kernel(const u16* src, int64_t total, float* dst) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x)
     dst[i] = f16_to_f32(src[i]);
@@ -504,6 +565,14 @@ hipError_t value_bounds(const float* v, int64_t n, unsigned* keys, hipStream_t s
   if (e != hipSuccess || n <= 0) return e;
   const int blocks = (int)std::min<int64_t>((n + 255) / 256, 2048);
   value_bounds_kernel<<<blocks, 256, 0, s>>>(v, n, keys);
+  return hipGetLastError();
+}
+
+hipError_t kth_thresholds(const float* scores, int64_t lds, int64_t nq, int64_t C, int k, float margin, float* th,
+                          hipStream_t s) {
+  if (nq <= 0) return hipSuccess;
+  if (k < 1 || k > KTH_MAX || C < k) return hipErrorInvalidValue;
+  kth_threshold_kernel<<<(unsigned)nq, 256, 0, s>>>(scores, lds, C, k, margin, th);
   return hipGetLastError();
 }
 

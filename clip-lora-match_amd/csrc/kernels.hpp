@@ -199,6 +199,10 @@ hipError_t gather_rows(const void* src, int64_t src_stride, const int64_t* idx, 
                        void* dst, int64_t dst_stride, bool scatter, hipStream_t s);
 // th[q] = ts[q * ld + k - 1] - margin
 hipError_t filter_thresholds(const float* ts, int64_t ld, int64_t nq, int k, float margin, float* th, hipStream_t s);
+// th[q] = (k-th largest of scores row q [C], duplicates counted) - margin, bit-identical to
+// topk_rows + filter_thresholds; k <= 8, C >= k
+hipError_t kth_thresholds(const float* scores, int64_t lds, int64_t nq, int64_t C, int k, float margin, float* th,
+                          hipStream_t s);
 // keys[0] / keys[1] = order key (float_key) of min / max over v[0, n); a NaN anywhere makes the
 // decoded min or max NaN. keys: 2 device u32
 hipError_t value_bounds(const float* v, int64_t n, unsigned* keys, hipStream_t s);

@@ -225,6 +225,12 @@ int clm_gemm_num_configs(void);
  * as two kernels instead of the fused one, bit 5 (32) = encode every padded caption row
  * instead of each caption's live rows (all: same embeddings, for parity tests). */
 void clm_debug_set(int flags);
+/* sampled-search thresholds (the bounded search's step 1 over the sample-score rows):
+ * th[q] = (k-th largest of scores[q, 0:C), duplicates counted) - margin, scores [nq, lds] f32,
+ * device pointers. method 0: one streaming pass (k <= 8), 1: radix top-k select + gather (the
+ * general path, k <= 1024); both give the same bits. */
+int clm_topk_threshold(int hip_device, const float* scores, int64_t lds, int64_t nq, int64_t C, int k,
+                       float margin, int method, float* th, void* stream);
 /* attention over qkv [B*T, 3*H*64] (q pre-scaled), out [B*T, ldo] (device pointers) */
 int clm_attention(int hip_device, int dtype, int causal, const void* qkv, void* out, int64_t ldo,
                   int B, int T, int H, void* stream);

@@ -376,6 +376,33 @@ def test_filter_skip_test_edge_cases(monkeypatch, case):
     idx.close()
 
 
+@pytest.mark.parametrize("k", [1, 3, 5, 8])
+@pytest.mark.parametrize("shape", [(300, 195_328, 195_328, 0), (64, 10_001, 10_240, 0), (32, 8191, 8192, 1)])
+def test_topk_threshold_streaming_equals_radix(k, shape):
+    """The sampled search's thresholds: the one-pass streaming k-th value (method 0) equals the
+    radix top-k select + gather (method 1) bit for bit, and numpy's k-th largest minus the margin,
+    on rows with heavy duplicates, +-inf, ragged C (scalar tail) and a misaligned row base."""
+    from clip_lora_match_amd import _capi as C
+    nq, c, lds, shift = shape
+    g = torch.Generator(device="cuda").manual_seed(k * 7 + c)
+    buf = torch.randn((nq * lds + shift,), generator=g, device="cuda")
+    sc = buf[shift:].view(nq, lds)
+    sc[: nq // 3] = torch.round(sc[: nq // 3] * 4) / 4          # few distinct values: tie groups
+    sc[nq // 3, :16] = float("inf")
+    sc[nq // 3 + 1] = -float("inf")
+    sc[nq // 3 + 1, 5] = 2.0
+    th = [torch.empty(nq, device="cuda") for _ in range(2)]
+    margin = 0.003
+    L = C.lib()
+    for m in (0, 1):
+        C.check(L.clm_topk_threshold(0, C.ptr(sc), lds, nq, c, k, margin, m, C.ptr(th[m]), None))
+    torch.cuda.synchronize()
+    assert torch.equal(th[0].view(torch.int32), th[1].view(torch.int32))
+    ref = np.sort(sc[:, :c].cpu().numpy(), axis=1)[:, c - k] - np.float32(margin)
+    assert np.array_equal(th[0].cpu().numpy(), ref.astype(np.float32))
+    assert L.clm_topk_threshold(0, C.ptr(sc), lds, nq, c, 9, margin, 0, C.ptr(th[0]), None) != 0
+
+
 # ---- query fusion (seeker_service.py:84-186) ------------------------------------------------
 def _unit_rows(n, d, seed):
     x = np.random.default_rng(seed).standard_normal((n, d)).astype(np.float32)
