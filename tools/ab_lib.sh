@@ -13,7 +13,7 @@ for rep in 1 2 3; do
     [ -f ab/_capi_$lib.py ] && cp ab/_capi_$lib.py clip-lora-match_amd/_capi.py
     env $envs timeout -k 10 300 python bench.py --no-search --no-cpu-baseline --no-l14 --no-varlen --no-index-build --no-unmerged --no-parity-mode ${BENCH_ARGS:-} > gpurun_out/abl/$name.$rep.json 2> gpurun_out/abl/$name.$rep.err
     rc=$?; [ $rc -eq 0 ] || { tail -5 gpurun_out/abl/$name.$rep.err; restore; exit $rc; }
-    python -c "import json; d=json.load(open('gpurun_out/abl/$name.$rep.json')); print('$name', $rep, d['value'], d['ms_per_step'], d["roofline"].get("achieved"))"
+    python -c "import json; d=json.load(open('gpurun_out/abl/$name.$rep.json')); print('$name', $rep, d['value'], d['ms_per_step'], d.get('roofline',{}).get('achieved'))"
   done
 done
 restore
