@@ -322,6 +322,9 @@ int pick_config(int epi, int M, int N) {
     forced = e ? atoi(e) : -1;
   }
   if (forced >= 0 && forced < NCFG) return forced;
+  // the search's filter GEMM (K = 512, no stores): G2's loop, 256 x 192 -- configs[4] search
+  // 95.9 k QPS vs 86.4 k with gemm_kernel 256 x 256 (profiles/r04_v7_search_cfg_ab.txt)
+  if (epi == EPI_FILTER) return pick_from(MODELS_G2, M, N);
   if (epi != EPI_GELU) return pick_from(MODELS, M, N);
   // Large M (>= 4 full rounds of 256 x 256 tiles, e.g. ViT-L/14@336 batch 128: fc1 73,856 x 4,096):
   // quantisation no longer favours G2's narrower tiles: gemm_kernel 256 x 256 takes 636 us there
