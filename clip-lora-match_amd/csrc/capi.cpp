@@ -1761,7 +1761,10 @@ int clm_index_search(clm_index* x, const void* q, int q_dtype, int64_t nq, int k
     r = search_scan(x, true, q16, qinv, q32, qn, nq, k, osc, oix, st);
     x->search_stats[1] += nq;
   } else {
-    const int64_t S = round_up(std::max<int64_t>(8192, (int64_t)k * N / 256), 256);
+    // sample of S rows: the k-th best of the sample ranks ~k * N / S = 256 in the index, so ~256
+    // candidates per query ($CLM_SAMPLE_DIV replaces the 256: A/B only)
+    static const int64_t sdiv = getenv("CLM_SAMPLE_DIV") ? std::max<int64_t>(16, atoll(getenv("CLM_SAMPLE_DIV"))) : 256;
+    const int64_t S = round_up(std::max<int64_t>(8192, (int64_t)k * N / sdiv), 256);
     const bool sampled = !(e_exact && atoi(e_exact)) && k <= 256 && N >= 4 * S && S <= (1 << 18);
     r = search_bounded(x, sampled, S, q16, qinv, q32, qn, nq, k, osc, oix, st);
   }
