@@ -1586,8 +1586,10 @@ static int search_bounded(clm_index* x, bool sampled, int64_t S, const u16* q16,
   // (default 8192) and at most a quarter of the free HBM.
   static const int64_t ws_mb = getenv("CLM_SEARCH_WS_MB") ? atoll(getenv("CLM_SEARCH_WS_MB")) : 8192;
   // query-block cap ($CLM_SEARCH_QB, A/B): a block's fp16 queries are re-read from L2 by every
-  // index tile, so 4096 x 512 (4 MB) fills an XCD's L2
-  static const int64_t qb_cap = getenv("CLM_SEARCH_QB") ? std::max<int64_t>(64, atoll(getenv("CLM_SEARCH_QB"))) : 4096;
+  // index tile; with the filter GEMM on G2 tiles 2560 beats 4096 (10 k queries: 100.5 k vs 97.7 k
+  // QPS, profiles/r04_v7_search_qb_ab.txt), and the blocks are balanced (a cap of 4096 gives
+  // 10 k = 3392 + 3392 + 3216 instead of 4096 + 4096 + 1808)
+  static const int64_t qb_cap = getenv("CLM_SEARCH_QB") ? std::max<int64_t>(64, atoll(getenv("CLM_SEARCH_QB"))) : 2560;
   int64_t nqb = std::min<int64_t>(nq, qb_cap);
   if (sampled) {
     size_t fr = 0, tot = 0;
@@ -1595,6 +1597,11 @@ static int search_bounded(clm_index* x, bool sampled, int64_t S, const u16* q16,
     if (hipMemGetInfo(&fr, &tot) == hipSuccess) cap_b = std::min<int64_t>(cap_b, (int64_t)(fr / 4));
     else (void)hipGetLastError();
     nqb = std::min<int64_t>(std::min<int64_t>(nq, qb_cap), std::max<int64_t>(256, cap_b / ((int64_t)S * 4)));
+  }
+  {   // balance: the same number of blocks, equal sizes (multiples of 64 rows while that stays <= the cap)
+    const int64_t nblk = (nq + nqb - 1) / nqb;
+    const int64_t even = (nq + nblk - 1) / nblk;
+    nqb = std::min<int64_t>(nqb, round_up(even, 64));
   }
   size_t off = 0;
   auto take = [&](size_t bytes) { size_t o = off; off = round_up(off + bytes, 256); return o; };
