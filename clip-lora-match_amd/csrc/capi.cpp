@@ -1508,7 +1508,11 @@ static int overflow_wide(clm_index* x, const std::vector<int64_t>& qs, const std
     gf.cnt = cnt; gf.cand_s = (float*)(w + p_cs); gf.cand_i = (int64_t*)(w + p_ci); gf.cap = (int)cap_max;
     gf.base = x->offset; gf.m_fastest = 1;
     gf.cbound = inv_keys_of(x, st);
-    if ((e = gemm(false, EPI_FILTER, gf, st)) != hipSuccess) break;
+    // these queries' lists overflowed: appends dominate this pass, where gemm_kernel's 256 x 256
+    // FILTER epilogue beats G2's (near-duplicate leg 73.7 k vs 66.0 k QPS,
+    // profiles/r04_v7_neardup_ab.txt)
+    static const int ocfg = getenv("CLM_GEMM_CFG") ? -1 : 1;
+    if ((e = gemm_cfg(false, EPI_FILTER, ocfg, gf, st)) != hipSuccess) break;
     if ((e = rescore_wide((const int64_t*)(w + p_ci), cnt, cap_max, (const float*)(w + p_q32),
                           (const double*)(w + p_qn), dim, xrows, !x->rows32, x->offset, ng, k, (float*)(w + p_ps),
                           (int64_t*)(w + p_pi), st)) != hipSuccess) break;
