@@ -84,6 +84,8 @@ for name in only:
         variants[f"c{cfg}_full"] = (lambda c: lambda: run(c, bufs[c]))(cfg)
         variants[f"c{cfg}_noepi"] = (lambda c: lambda: run(c, bufs[c], 1))(cfg)
         variants[f"c{cfg}_nostore"] = (lambda c: lambda: run(c, bufs[c], 2))(cfg)
+        for dv in filter(None, os.environ.get("PROBE_DBG", "").split(",")):   # extra debug-flag variants
+            variants[f"c{cfg}_dbg{dv}"] = (lambda c, v: lambda: run(c, bufs[c], v))(cfg, int(dv))
     for fn in variants.values():
         fn()
     torch.cuda.synchronize()
