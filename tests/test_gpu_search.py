@@ -376,6 +376,28 @@ def test_filter_skip_test_edge_cases(monkeypatch, case):
     idx.close()
 
 
+def test_bounded_search_many_query_blocks(monkeypatch):
+    """5,121 queries through the sampled bounded search: three balanced query blocks (1728, 1728,
+    1665 rows; the filter GEMM on G2 tiles of both shapes) return exactly what the full exact scan
+    returns."""
+    monkeypatch.setenv("CLM_SEARCH_BOUNDED", "1")
+    n, dim, nq, k = 40_000, 128, 5121, 5   # n >= 4 x the 8192-row sample: the sampled path serves
+    g = torch.Generator(device="cuda").manual_seed(31)
+    rows = torch.randn((n, dim), generator=g, device="cuda").half()
+    q = torch.randn((nq, dim), generator=g, device="cuda").half()
+    q[:64] = rows[torch.arange(64, device="cuda") * 600]   # exact hits at rank 0
+    idx = CosineIndex(dim, capacity=n)
+    idx.append(rows)
+    s, i = idx.search(q, k)
+    assert idx.stats()["filtered"] + idx.stats()["overflow"] >= nq
+    assert torch.equal(i[:64, 0], torch.arange(64, device="cuda") * 600)
+    monkeypatch.delenv("CLM_SEARCH_BOUNDED")
+    monkeypatch.setenv("CLM_SEARCH_FULL", "1")
+    s_ref, i_ref = idx.search(q, k)
+    assert torch.equal(i, i_ref) and torch.equal(s, s_ref)
+    idx.close()
+
+
 @pytest.mark.parametrize("k", [1, 3, 5, 8])
 @pytest.mark.parametrize("shape", [(300, 195_328, 195_328, 0), (64, 10_001, 10_240, 0), (32, 8191, 8192, 1)])
 def test_topk_threshold_streaming_equals_radix(k, shape):
