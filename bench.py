@@ -97,6 +97,7 @@ def parse_args(argv=None):
     ap.add_argument("--split", type=int, default=0, help="sub-batches per tower in encode_pair (0 = library default)")
     ap.add_argument("--no-trace", action="store_true", help="skip the rocprofv3 kernel trace of the headline step")
     ap.add_argument("--trace-child", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--no-graph", action="store_true", help="two tower streams without the hipGraph replay (A/B)")
     return ap.parse_args(argv)
 
 
@@ -936,7 +937,7 @@ def main():
             model.encode_pixels(imgs, out=emb[:B])
             model.encode_ids(ids, out=emb[B:])
         else:   # towers concurrently on two streams, replayed from a captured hipGraph
-            model.encode_pair(imgs, ids, out_img=emb[:B], out_txt=emb[B:], graph=True, split=args.split)
+            model.encode_pair(imgs, ids, out_img=emb[:B], out_txt=emb[B:], graph=not args.no_graph, split=args.split)
         if world > 1:
             torch.distributed.all_gather_into_tensor(gathered, emb)
 
