@@ -86,7 +86,7 @@ def _worker(rank, world, port, n, dim, nq, k, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,n", [(2, 101), (3, 64), (2, 1)])
+@pytest.mark.parametrize("world,n", [(2, 101), (3, 64), (2, 1), (4, 3), (8, 37)])
 def test_sharded_build_and_search_gloo(world, n):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
