@@ -16,7 +16,7 @@ SHAPES = {"v_qkv": (B * 50, 2304, 768, 0), "v_out": (B * 50, 768, 768, 2), "v_fc
           "v_fc2": (B * 50, 768, 3072, 2), "t_qkv": (B * 77, 1536, 512, 0), "t_out": (B * 77, 512, 512, 2),
           "t_fc1": (B * 77, 2048, 512, 1), "t_fc2": (B * 77, 512, 2048, 2), "odd": (1000, 200, 192, 1),
           "l_fc1": (128 * 577, 4096, 1024, 1), "l_fc2": (128 * 577, 1024, 4096, 2),
-          "l_qkv": (128 * 577, 3072, 1024, 0), "sq8k": (8192, 8192, 8192, 0)}
+          "l_qkv": (128 * 577, 3072, 1024, 0), "l_out": (128 * 577, 1024, 1024, 2), "sq8k": (8192, 8192, 8192, 0)}
 cfgs = [int(x) for x in sys.argv[1].split(",")] if len(sys.argv) > 1 else [12, 13, 14, 15, 16]
 only = sys.argv[2].split(",") if len(sys.argv) > 2 else ["v_fc1", "t_fc1", "v_fc2", "t_fc2", "v_out", "t_out", "v_qkv"]
 dev = torch.device("cuda", 0)
