@@ -90,7 +90,8 @@ def parse_args(argv=None):
     ap.add_argument("--no-unmerged", action="store_true", help="skip the unmerged (hot-swappable) LoRA leg")
     ap.add_argument("--no-index-build", action="store_true", help="skip the configs[2] index-build leg")
     ap.add_argument("--index-images", type=int, default=1_000_000, help="images of the configs[2] index build")
-    ap.add_argument("--index-batch", type=int, default=512)
+    ap.add_argument("--index-batch", type=int, default=1280,
+                    help="encode batch of the configs[2] leg (1280: profiles/r04_v8_index_batch_sweep.txt)")
     ap.add_argument("--no-persist", action="store_true", help="skip the search index shard save / load timing")
     ap.add_argument("--no-near-dup", action="store_true", help="skip the near-duplicate-rows search leg")
     ap.add_argument("--sequential", action="store_true", help="towers back to back on one stream, no graph")
