@@ -225,6 +225,10 @@ struct clm_index {
   // queries served by: [0] sampled bounded search, [1] the full exact scan, [2] overflow re-runs,
   // [3] bounded search with the chunked fp16 scan as step 1
   int64_t search_stats[4] = {0, 0, 0, 0};
+  // the last bounded search had most of its candidate lists overflow (near-duplicate rows): the
+  // next one runs its filter pass on gemm_kernel's 256 x 256 tiles, whose FILTER epilogue is the
+  // faster one when appends dominate (same candidates either way)
+  bool dense_hits = false;
 };
 
 namespace {
@@ -1205,6 +1209,7 @@ int clm_index_append(clm_index* x, const void* rows, int dtype, int64_t n, void*
   if (r) return r;
   x->samp_n = -1;   // the threshold sample is rebuilt from the new row set
   x->inv_keys_n = -1;
+  x->dense_hits = false;
   if (dtype == CLM_F32 && !x->rows32) {
     // first fp32 rows: keep an fp32 copy from now on; the rows so far were fp16 as given
     if (hipMalloc(&x->rows32, (size_t)x->cap * x->dim * sizeof(float)) != hipSuccess) {
@@ -1282,6 +1287,7 @@ int clm_index_import(clm_index* x, const uint16_t* rows16, const float* inv, con
   if (r) return r;
   x->samp_n = -1;
   x->inv_keys_n = -1;
+  x->dense_hits = false;
   const size_t cnt = (size_t)n * x->dim;
   if (rows32 && !x->rows32) {   // as clm_index_append: the first fp32 rows start the fp32 copy
     if (hipMalloc(&x->rows32, (size_t)x->cap * x->dim * sizeof(float)) != hipSuccess) {
@@ -1311,6 +1317,7 @@ int clm_index_reset(clm_index* x) {
   x->n = 0;
   x->samp_n = -1;   // never reuse a sample of the previous rows
   x->inv_keys_n = -1;
+  x->dense_hits = false;
   return CLM_OK;
 }
 
@@ -1656,7 +1663,8 @@ static int search_bounded(clm_index* x, bool sampled, int64_t S, const u16* q16,
     gf.m_fastest = 1;
     gf.cbound = inv_keys_of(x, st);
     gf.debug = g_gemm_debug & 3;   // diagnostics only ($CLM_GEMM_DEBUG): main loop alone / stores dropped
-    KCHK(gemm(false, EPI_FILTER, gf, st));
+    static const bool cfg_forced = getenv("CLM_GEMM_CFG") != nullptr;
+    KCHK(gemm_cfg(false, EPI_FILTER, x->dense_hits && !cfg_forced ? 1 : -1, gf, st));
     KCHK(rescore_select(cs, ci, cnt, CAND_CAP, q32 + q0 * dim, qn + q0, dim, xrows, !x->rows32, x->offset,
                         RESCORE_MARGIN, nb, k, osc + q0 * k, oix + q0 * k, st));
     hcnt.resize(nb);
@@ -1669,6 +1677,7 @@ static int search_bounded(clm_index* x, bool sampled, int64_t S, const u16* q16,
       }
   }
   x->search_stats[sampled ? 0 : 3] += nq - (int64_t)overflow.size();
+  x->dense_hits = 2 * (int64_t)overflow.size() > nq;
   if (overflow.empty()) return CLM_OK;
   // Candidate lists beyond CAND_CAP (near-duplicate rows inside the window). Lists of up to
   // (SORT_MAX / k) chunks are rebuilt whole by a second filter pass over just those queries and
