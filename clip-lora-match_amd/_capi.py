@@ -71,6 +71,7 @@ def lib():
         "clm_encode_text": (c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p, c_int, c_int, c_void_p]),
         "clm_encode_pair": (c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p, c_int, c_int, c_void_p, c_void_p,
                                     c_int, c_int, c_int, c_void_p]),
+        "clm_pair_path": (c_int, [c_void_p]),
         "clm_index_create": (c_int, [c_int, c_int64, c_int, POINTER(c_void_p)]),
         "clm_index_destroy": (c_int, [c_void_p]),
         "clm_index_append": (c_int, [c_void_p, c_void_p, c_int, c_int64, c_void_p]),
@@ -119,7 +120,7 @@ def lib():
 
 EXPORTED = (
     "clm_ctx_create", "clm_ctx_destroy", "clm_load_tensor", "clm_finalize", "clm_set_lora_enabled", "clm_set_lora",
-    "clm_encode_image", "clm_encode_text", "clm_encode_pair", "clm_index_create", "clm_index_destroy", "clm_index_append",
+    "clm_encode_image", "clm_encode_text", "clm_encode_pair", "clm_pair_path", "clm_index_create", "clm_index_destroy", "clm_index_append",
     "clm_index_size", "clm_index_reset", "clm_index_set_offset", "clm_index_read", "clm_index_search", "clm_index_stats",
     "clm_index_stats2",
     "clm_cosine_scores", "clm_topk_merge", "clm_topk_threshold", "clm_l2_normalize", "clm_fuse_queries", "clm_resize_crop", "clm_synth_images", "clm_index_has_f32", "clm_index_export", "clm_index_import",

@@ -159,6 +159,7 @@ struct clm_ctx {
   hipEvent_t ev_fork = nullptr, ev_done = nullptr;
   typedef std::tuple<const void*, int, int, const void*, int, int, void*, void*, int, int, int> PairKey;
   std::map<PairKey, hipGraphExec_t> graphs;
+  int last_pair_path = -1;   // clm_pair_path: 0 = two tower streams, 1 = grouped launches
   // kernel timing (clm_prof_*): events recorded on the launch stream
   bool prof = false;
   std::vector<hipEvent_t> ev_pool;
@@ -561,6 +562,162 @@ bool fused_attention(int T, int H, int d, int K) {
   return v == 1 && !(g_gemm_debug & 16) && gemm_attn_supported(T, H, d, K);
 }
 
+// Per-call state of one tower's encoder pass (run_layers / run_layers_pair).
+struct LayerRun {
+  Tower* T;
+  int B, S;
+  bool causal, vl, bf;
+  const int32_t* ids;
+  const int* mdev;            // varlen: device-resident live row count (T.vl_counts)
+  double Mx, attn_pairs;      // executed rows / attention pairs (profiling)
+};
+
+int make_run(clm_ctx* c, Tower& T, int B, int S, bool causal, const int32_t* ids, bool vl, hipStream_t st,
+             LayerRun* r) {
+  *r = LayerRun{&T, B, S, causal, vl, c->bf16(T.vision), ids, vl ? T.vl_counts : nullptr, (double)B * S,
+                (double)B * S * S};
+  // varlen (packed live text rows): the row-wise kernels read the live row count from
+  // T.vl_counts; the profiled pass (no graph, may sync) counts the executed rows and attention pairs
+  if (vl && c->prof) {
+    std::vector<int> lens(B);
+    HIPCHK(hipMemcpyAsync(lens.data(), T.vl_lens, (size_t)B * 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    r->Mx = r->attn_pairs = 0;
+    for (int v : lens) { r->Mx += v; r->attn_pairs += (double)v * v; }
+  }
+  return CLM_OK;
+}
+
+// layer l's fused q/k/v + attention problem of one tower (gemm_attn / gemm_attn_varlen arguments)
+AttnProblem attn_problem(const LayerRun& R, int l) {
+  Tower& T = *R.T;
+  const LayerW& Lw = T.layers[l];
+  AttnProblem p{T.X, T.ldx, Lw.w_qkv, Lw.k_qkv, Lw.b_qkv, T.O, T.ldo, R.B, R.S, T.H, T.d, Lw.k_qkv,
+                nullptr, nullptr, nullptr, nullptr};
+  if (R.vl) { p.lens = T.vl_lens; p.offs = T.vl_offs; p.tiles = T.vl_tiles; p.counts = T.vl_counts; }
+  return p;
+}
+double attn_flops(const LayerRun& R, int l) {
+  const Tower& T = *R.T;
+  return 2.0 * R.Mx * 3 * T.d * T.layers[l].k_qkv + 4.0 * T.H * R.attn_pairs * 64;
+}
+
+// layer l's q/k/v projection + attention of one tower: T.X -> T.O
+int attn_step(clm_ctx* c, const LayerRun& R, int l, hipStream_t st) {
+  Tower& T = *R.T;
+  LayerW& Lw = T.layers[l];
+  const bool bf = R.bf;
+  GemmArgs g{};
+  g.A = T.X; g.lda = T.ldx; g.M = R.B * R.S; g.N = 3 * T.d; g.K = Lw.k_qkv; g.out = T.QKV; g.ldo = 3 * T.d;
+  g.W = Lw.w_qkv; g.ldw = Lw.k_qkv; g.bias = Lw.b_qkv;
+  if (R.vl) {   // packed live rows of variable-length captions
+    PROF(CLM_PROF_GEMM, attn_flops(R, l));
+    KCHK(gemm_attn_varlen(bf, R.causal, g.A, g.lda, g.W, g.ldw, g.bias, T.O, T.ldo, R.B, R.S, T.H, T.d, g.K,
+                          T.vl_lens, T.vl_offs, T.vl_tiles, T.vl_counts, st));
+  } else if (fused_attention(R.S, T.H, T.d, g.K)) {
+    // one launch: the q/k/v GEMM's tiles attend their own sequences (GEMM + attention FLOPs)
+    PROF(CLM_PROF_GEMM, attn_flops(R, l));
+    KCHK(gemm_attn(bf, R.causal, g.A, g.lda, g.W, g.ldw, g.bias, T.O, T.ldo, R.B, R.S, T.H, T.d, g.K, st));
+  } else {
+    { PROF(CLM_PROF_GEMM, 2.0 * g.M * g.N * g.K); KCHK(gemm(bf, EPI_STORE, g, st)); }
+    { PROF(CLM_PROF_ATTN, 4.0 * R.B * T.H * (double)R.S * R.S * 64);
+      KCHK(attention(bf, R.causal, T.QKV, 3 * T.d, T.O, T.ldo, R.B, R.S, T.H, T.d, st)); }
+  }
+  return CLM_OK;
+}
+
+// the pruned last layer's residual GEMMs have only B (pooled) rows: K is split into slices of
+// >= 4 K-steps (a fixed count per shape, so a row's bits do not depend on B), partials in the
+// QKV workspace, which is idle by then (B * S rows * 3d 16-bit values); 75 µs of idle chip per
+// launch before (profiles/r02_v5_pooled_splitk_ab.txt)
+int pooled_resid(clm_ctx* c, const LayerRun& R, GemmArgs& g, hipStream_t st) {
+  const int nk = g.K / 64;
+  int slices = 1;
+  for (int sl = nk / 4; sl >= 2; --sl)
+    if (nk % sl == 0 && gemm_splitk_ws_bytes(1, g.N, sl) <= (size_t)R.S * 3 * R.T->d * 2) { slices = sl; break; }
+  PROF(CLM_PROF_GEMM, 2.0 * g.M * g.N * g.K);
+  if (slices > 1) KCHK(gemm_splitk_resid(R.bf, g, slices, (float*)R.T->QKV, st));
+  else KCHK(gemm_cfg(R.bf, EPI_RESID, GEMM_CFG_SPLITK, g, st));
+  return CLM_OK;
+}
+
+// The four row-wise GEMMs and two LayerNorms of layer l after its attention, as (M rows of) one
+// tower: out_proj (+= h), LN2 -> X, fc1 (GELU) -> Hm, fc2 (+= h), next layer's LN1 -> X.
+struct PostOps {
+  GemmArgs out, fc1, fc2;
+  LnArgs ln2, ln1;
+  bool has_ln1;
+  double rows;   // executed rows (profiling)
+};
+PostOps post_ops(clm_ctx* c, const LayerRun& R, int l, int64_t M, float* h, u16* O, bool pooled) {
+  Tower& T = *R.T;
+  LayerW& Lw = T.layers[l];
+  const int* mdev = pooled ? nullptr : R.mdev;
+  PostOps p{};
+  p.rows = pooled ? (double)M : R.Mx;
+  GemmArgs& g = p.out;
+  g.A = O; g.lda = T.ldo; g.W = Lw.w_out; g.ldw = Lw.k_out; g.M = (int)M; g.N = T.d; g.K = Lw.k_out;
+  g.out = h; g.ldo = T.d; g.bias = Lw.b_out; g.m_dev = mdev;
+  p.ln2 = ln_into_x(c, T, M, Lw.ln2_g, Lw.ln2_b, Lw.a_fc1, Lw.r_fc1, h);
+  p.ln2.m_dev = mdev;
+  GemmArgs& f = p.fc1;
+  f.A = T.X; f.lda = T.ldx; f.M = (int)M; f.N = T.mlp; f.K = Lw.k_fc1; f.out = T.Hm; f.ldo = T.ldm;
+  f.W = Lw.w_fc1; f.ldw = Lw.k_fc1; f.bias = Lw.b_fc1; f.m_dev = mdev;
+  GemmArgs& f2 = p.fc2;
+  f2.A = T.Hm; f2.lda = T.ldm; f2.W = Lw.w_fc2; f2.ldw = Lw.k_fc2; f2.M = (int)M; f2.N = T.d; f2.K = Lw.k_fc2;
+  f2.out = h; f2.ldo = T.d; f2.bias = Lw.b_fc2; f2.m_dev = mdev;
+  p.has_ln1 = l + 1 < T.L;
+  if (p.has_ln1) {
+    LayerW& Ln = T.layers[l + 1];
+    p.ln1 = ln_into_x(c, T, M, Ln.ln1_g, Ln.ln1_b, Ln.a_qkv, Ln.r_qkv);
+    p.ln1.m_dev = mdev;
+  }
+  return p;
+}
+
+// layer l after its attention, one tower. The last layer is pruned to the pooled rows
+// (prune_last_layer): they are gathered into T.hc / T.Oc first and *pooled_rows is set.
+int post_attn_step(clm_ctx* c, const LayerRun& R, int l, bool* pooled_rows, hipStream_t st) {
+  Tower& T = *R.T;
+  LayerW& Lw = T.layers[l];
+  const bool bf = R.bf;
+  const bool pooled = prune_last_layer() && l + 1 == T.L;
+  int64_t M = (int64_t)R.B * R.S;
+  float* h = T.h;
+  u16* O = T.O;
+  if (pooled) {
+    { PROF(CLM_PROF_OTHER, (double)R.B * T.d * 6.0);
+      KCHK(gather_pooled(T.h, T.d, T.O, T.ldo, R.B, R.S, T.d, R.ids, c->desc.eos_token_id, T.hc, T.Oc, T.ldo, st,
+                         R.vl ? T.vl_offs : nullptr)); }
+    M = R.B;
+    h = T.hc;
+    O = T.Oc;
+    *pooled_rows = true;
+  }
+  PostOps p = post_ops(c, R, l, M, h, O, pooled);
+  if (Lw.r_out) { PROF(CLM_PROF_OTHER, 2.0 * M * T.d + 4.0 * Lw.r_out * T.d);
+    KCHK(lora_down(bf, O, T.ldo, (int)M, T.d, Lw.a_out, Lw.r_out, RPAD, st)); }
+  if (pooled) {
+    int r = pooled_resid(c, R, p.out, st);
+    if (r) return r;
+  } else {
+    PROF(CLM_PROF_GEMM, 2.0 * p.rows * p.out.N * p.out.K); KCHK(gemm(bf, EPI_RESID, p.out, st));
+  }
+  { PROF(CLM_PROF_LN, p.rows * T.d * 6.0); KCHK(layernorm(bf, p.ln2, st)); }
+  { PROF(CLM_PROF_GEMM, 2.0 * p.rows * p.fc1.N * p.fc1.K);   // pooled rows: 128 x 64 tiles (4 waves) fill the chip
+    KCHK(pooled ? gemm_cfg(bf, EPI_GELU, GEMM_CFG_SPLITK, p.fc1, st) : gemm(bf, EPI_GELU, p.fc1, st)); }
+  if (Lw.r_fc2) { PROF(CLM_PROF_OTHER, 2.0 * M * T.mlp + 4.0 * Lw.r_fc2 * T.mlp);
+    KCHK(lora_down(bf, T.Hm, T.ldm, (int)M, T.mlp, Lw.a_fc2, Lw.r_fc2, RPAD, st)); }
+  if (pooled) {
+    int r = pooled_resid(c, R, p.fc2, st);
+    if (r) return r;
+  } else {
+    PROF(CLM_PROF_GEMM, 2.0 * p.rows * p.fc2.N * p.fc2.K); KCHK(gemm(bf, EPI_RESID, p.fc2, st));
+  }
+  if (p.has_ln1) { PROF(CLM_PROF_LN, p.rows * T.d * 6.0); KCHK(layernorm(bf, p.ln1, st)); }
+  return CLM_OK;
+}
+
 // encoder layers on the residual stream T.h; the first layer's LN1 output must already be in T.X.
 // Returns with the pooled rows in T.hc (pruned: *pooled_rows = true) or all rows in T.h.
 // (LayerNorm folded into the next GEMM -- producer moments in the residual epilogue, consumer
@@ -568,109 +725,75 @@ bool fused_attention(int T, int H, int d, int K) {
 // removed: profiles/r02_v2_ln_fold_ab.txt.)
 int run_layers(clm_ctx* c, Tower& T, int B, int S, bool causal, const int32_t* ids, bool* pooled_rows,
                hipStream_t st, bool vl = false) {
-  const bool bf = c->bf16(T.vision);
-  const bool prune = prune_last_layer();
   *pooled_rows = false;
-  // varlen (packed live text rows): the row-wise kernels read the live row count from
-  // T.vl_counts; the profiled pass (no graph, may sync) counts the executed rows and attention pairs
-  const int* mdev = vl ? T.vl_counts : nullptr;
-  double Mx = (double)B * S, attn_pairs = (double)B * S * S;
-  if (vl && c->prof) {
-    std::vector<int> lens(B);
-    HIPCHK(hipMemcpyAsync(lens.data(), T.vl_lens, (size_t)B * 4, hipMemcpyDeviceToHost, st));
-    HIPCHK(hipStreamSynchronize(st));
-    Mx = attn_pairs = 0;
-    for (int v : lens) { Mx += v; attn_pairs += (double)v * v; }
+  LayerRun R;
+  int r = make_run(c, T, B, S, causal, ids, vl, st, &R);
+  for (int l = 0; !r && l < T.L; ++l) {
+    r = attn_step(c, R, l, st);
+    if (!r) r = post_attn_step(c, R, l, pooled_rows, st);
   }
-  // the pruned last layer's residual GEMMs have only B (pooled) rows: K is split into slices of
-  // >= 4 K-steps (a fixed count per shape, so a row's bits do not depend on B), partials in the
-  // QKV workspace, which is idle by then (B * S rows * 3d 16-bit values); 75 µs of idle chip per
-  // launch before (profiles/r02_v5_pooled_splitk_ab.txt)
-  auto pooled_resid = [&](GemmArgs& g) -> int {
-    const int nk = g.K / 64;
-    int slices = 1;
-    for (int sl = nk / 4; sl >= 2; --sl)
-      if (nk % sl == 0 && gemm_splitk_ws_bytes(1, g.N, sl) <= (size_t)S * 3 * T.d * 2) { slices = sl; break; }
-    PROF(CLM_PROF_GEMM, 2.0 * g.M * g.N * g.K);
-    if (slices > 1) KCHK(gemm_splitk_resid(bf, g, slices, (float*)T.QKV, st));
-    else KCHK(gemm_cfg(bf, EPI_RESID, GEMM_CFG_SPLITK, g, st));
-    return CLM_OK;
-  };
-  for (int l = 0; l < T.L; ++l) {
-    LayerW& Lw = T.layers[l];
-    const bool last = l + 1 == T.L;
-    int64_t M = (int64_t)B * S;
-    GemmArgs g{};
-    g.A = T.X; g.lda = T.ldx; g.M = (int)M; g.N = 3 * T.d; g.K = Lw.k_qkv; g.out = T.QKV; g.ldo = 3 * T.d;
-    g.W = Lw.w_qkv; g.ldw = Lw.k_qkv; g.bias = Lw.b_qkv;
-    if (vl) {   // packed live rows of variable-length captions
-      PROF(CLM_PROF_GEMM, 2.0 * Mx * g.N * g.K + 4.0 * T.H * attn_pairs * 64);
-      KCHK(gemm_attn_varlen(bf, causal, g.A, g.lda, g.W, g.ldw, g.bias, T.O, T.ldo, B, S, T.H, T.d, g.K, T.vl_lens,
-                            T.vl_offs, T.vl_tiles, T.vl_counts, st));
-    } else if (fused_attention(S, T.H, T.d, g.K)) {
-      // one launch: the q/k/v GEMM's tiles attend their own sequences (GEMM + attention FLOPs)
-      PROF(CLM_PROF_GEMM, 2.0 * M * g.N * g.K + 4.0 * B * T.H * (double)S * S * 64);
-      KCHK(gemm_attn(bf, causal, g.A, g.lda, g.W, g.ldw, g.bias, T.O, T.ldo, B, S, T.H, T.d, g.K, st));
+  return r;
+}
+
+// Grouped mode of clm_encode_pair ($CLM_PAIR_GROUPED=1 or clm_debug_set bit 64; default off): the image and text towers'
+// layer l run as ONE launch per op on one stream -- fused q/k/v + attention (gemm_attn_pair),
+// out_proj and fc2 (gemm_pair RESID), LN2 / LN1 (layernorm_pair), fc1 (gemm_pair GELU) -- so the
+// two towers' tiles share the launches' rounds instead of two persistent kernels taking the chip
+// in turn (tile counts per launch: 400 + 462 RESID tiles over 512 slots, etc.). Every output bit
+// equals the two-stream path's (the pair kernels run each tower's tiles with that tower's code).
+// Layers 0 .. L-2 and the last layer's attention are grouped; the last layer's pruned row-wise
+// tail runs per tower (pair_launch puts each on its own stream).
+// Measured (round 5, B/32 batch 256, mixed): bit-identical, the pair kernels' summed time per step
+// 0.29 ms BELOW the two-stream step's kernels (the 160 x 128 RESID tiles pay once nothing else
+// wants the slots), but the step is 5.54 vs 4.92 ms: on two streams one tower's LayerNorms and
+// launch tails run under the other tower's GEMMs (~0.7 ms of kernel time hidden per step), which
+// one grouped chain cannot do (profiles/r05_v1_grouped_pair_ab.txt, r05_v1_grouped_pair_timeline.txt).
+bool pair_grouped() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("CLM_PAIR_GROUPED");
+    v = (e && atoi(e)) ? 1 : 0;
+  }
+  return v == 1 || (g_gemm_debug & 64);
+}
+int pair_persist() {   // $CLM_PAIR_PERSIST=1: persistent ranges instead of one tile per workgroup
+  static const int v = getenv("CLM_PAIR_PERSIST") ? atoi(getenv("CLM_PAIR_PERSIST")) : 0;
+  return v;
+}
+
+int run_layers_pair(clm_ctx* c, const LayerRun& V, const LayerRun& X, hipStream_t st) {
+  Tower& TV = *V.T;
+  Tower& TX = *X.T;
+  const int L = TV.L;
+  const bool fused = fused_attention(V.S, TV.H, TV.d, TV.layers[0].k_qkv) &&
+                     (X.vl || fused_attention(X.S, TX.H, TX.d, TX.layers[0].k_qkv));
+  for (int l = 0; l < L; ++l) {
+    if (fused) {
+      PROF(CLM_PROF_GEMM, attn_flops(V, l) + attn_flops(X, l));
+      KCHK(gemm_attn_pair(V.bf, X.bf, attn_problem(V, l), attn_problem(X, l), st));
     } else {
-      { PROF(CLM_PROF_GEMM, 2.0 * M * g.N * g.K); KCHK(gemm(bf, EPI_STORE, g, st)); }
-      { PROF(CLM_PROF_ATTN, 4.0 * B * T.H * (double)S * S * 64);
-        KCHK(attention(bf, causal, T.QKV, 3 * T.d, T.O, T.ldo, B, S, T.H, T.d, st)); }
-    }
-    float* h = T.h;
-    u16* O = T.O;
-    const bool pooled = prune && last;
-    if (pooled) {
-      { PROF(CLM_PROF_OTHER, (double)B * T.d * 6.0);
-        KCHK(gather_pooled(T.h, T.d, T.O, T.ldo, B, S, T.d, ids, c->desc.eos_token_id, T.hc, T.Oc, T.ldo, st,
-                           vl ? T.vl_offs : nullptr)); }
-      M = B;
-      h = T.hc;
-      O = T.Oc;
-      *pooled_rows = true;
-    }
-    if (Lw.r_out) { PROF(CLM_PROF_OTHER, 2.0 * M * T.d + 4.0 * Lw.r_out * T.d);
-      KCHK(lora_down(bf, O, T.ldo, (int)M, T.d, Lw.a_out, Lw.r_out, RPAD, st)); }
-    g = GemmArgs{};
-    g.A = O; g.lda = T.ldo; g.W = Lw.w_out; g.ldw = Lw.k_out; g.M = (int)M; g.N = T.d; g.K = Lw.k_out;
-    g.out = h; g.ldo = T.d; g.bias = Lw.b_out;
-    if (pooled) {
-      int r = pooled_resid(g);
+      int r = attn_step(c, V, l, st);
+      if (!r) r = attn_step(c, X, l, st);
       if (r) return r;
-    } else {
-      g.m_dev = mdev;
-      PROF(CLM_PROF_GEMM, 2.0 * Mx * g.N * g.K); KCHK(gemm(bf, EPI_RESID, g, st));
     }
-    {
-      LnArgs ln = ln_into_x(c, T, M, Lw.ln2_g, Lw.ln2_b, Lw.a_fc1, Lw.r_fc1, h);
-      if (!pooled) ln.m_dev = mdev;
-      PROF(CLM_PROF_LN, (pooled ? (double)M : Mx) * T.d * 6.0);
-      KCHK(layernorm(bf, ln, st));
-    }
-    g = GemmArgs{};
-    g.A = T.X; g.lda = T.ldx; g.M = (int)M; g.N = T.mlp; g.K = Lw.k_fc1; g.out = T.Hm; g.ldo = T.ldm;
-    g.W = Lw.w_fc1; g.ldw = Lw.k_fc1; g.bias = Lw.b_fc1;
-    if (!pooled) g.m_dev = mdev;
-    { PROF(CLM_PROF_GEMM, 2.0 * (pooled ? (double)M : Mx) * g.N * g.K);   // pooled rows: 128 x 64 tiles (4 waves) fill the chip
-      KCHK(pooled ? gemm_cfg(bf, EPI_GELU, GEMM_CFG_SPLITK, g, st) : gemm(bf, EPI_GELU, g, st)); }
-    if (Lw.r_fc2) { PROF(CLM_PROF_OTHER, 2.0 * M * T.mlp + 4.0 * Lw.r_fc2 * T.mlp);
-      KCHK(lora_down(bf, T.Hm, T.ldm, (int)M, T.mlp, Lw.a_fc2, Lw.r_fc2, RPAD, st)); }
-    g = GemmArgs{};
-    g.A = T.Hm; g.lda = T.ldm; g.W = Lw.w_fc2; g.ldw = Lw.k_fc2; g.M = (int)M; g.N = T.d; g.K = Lw.k_fc2;
-    g.out = h; g.ldo = T.d; g.bias = Lw.b_fc2;
-    if (pooled) {
-      int r = pooled_resid(g);
-      if (r) return r;
-    } else {
-      g.m_dev = mdev;
-      PROF(CLM_PROF_GEMM, 2.0 * Mx * g.N * g.K); KCHK(gemm(bf, EPI_RESID, g, st));
-    }
-    if (!last) {
-      LayerW& Ln = T.layers[l + 1];
-      LnArgs ln = ln_into_x(c, T, M, Ln.ln1_g, Ln.ln1_b, Ln.a_qkv, Ln.r_qkv);
-      ln.m_dev = mdev;
-      PROF(CLM_PROF_LN, Mx * T.d * 6.0);
-      KCHK(layernorm(bf, ln, st));
-    }
+    if (l + 1 == L) break;   // the last layer's tail: per tower (pooled rows)
+    PostOps pv = post_ops(c, V, l, (int64_t)V.B * V.S, TV.h, TV.O, false);
+    PostOps px = post_ops(c, X, l, (int64_t)X.B * X.S, TX.h, TX.O, false);
+    const LayerW &Lv = TV.layers[l], &Lx = TX.layers[l];
+    if (Lv.r_out) KCHK(lora_down(V.bf, TV.O, TV.ldo, pv.out.M, TV.d, Lv.a_out, Lv.r_out, RPAD, st));
+    if (Lx.r_out) KCHK(lora_down(X.bf, TX.O, TX.ldo, px.out.M, TX.d, Lx.a_out, Lx.r_out, RPAD, st));
+    { PROF(CLM_PROF_GEMM, 2.0 * (pv.rows * pv.out.N * pv.out.K + px.rows * px.out.N * px.out.K));
+      KCHK(gemm_pair(V.bf, X.bf, EPI_RESID, -1, pv.out, px.out, pair_persist(), st)); }
+    { PROF(CLM_PROF_LN, (pv.rows * TV.d + px.rows * TX.d) * 6.0);
+      KCHK(layernorm_pair(V.bf, X.bf, pv.ln2, px.ln2, st)); }
+    { PROF(CLM_PROF_GEMM, 2.0 * (pv.rows * pv.fc1.N * pv.fc1.K + px.rows * px.fc1.N * px.fc1.K));
+      KCHK(gemm_pair(V.bf, X.bf, EPI_GELU, -1, pv.fc1, px.fc1, pair_persist(), st)); }
+    if (Lv.r_fc2) KCHK(lora_down(V.bf, TV.Hm, TV.ldm, pv.fc2.M, TV.mlp, Lv.a_fc2, Lv.r_fc2, RPAD, st));
+    if (Lx.r_fc2) KCHK(lora_down(X.bf, TX.Hm, TX.ldm, px.fc2.M, TX.mlp, Lx.a_fc2, Lx.r_fc2, RPAD, st));
+    { PROF(CLM_PROF_GEMM, 2.0 * (pv.rows * pv.fc2.N * pv.fc2.K + px.rows * px.fc2.N * px.fc2.K));
+      KCHK(gemm_pair(V.bf, X.bf, EPI_RESID, -1, pv.fc2, px.fc2, pair_persist(), st)); }
+    { PROF(CLM_PROF_LN, (pv.rows * TV.d + px.rows * TX.d) * 6.0);
+      KCHK(layernorm_pair(V.bf, X.bf, pv.ln1, px.ln1, st)); }
   }
   return CLM_OK;
 }
@@ -690,8 +813,8 @@ Tower ws_view(const Tower& T0, int b0, int rows, int patches, int proj_dim) {
   return T;
 }
 
-int encode_image_chunk(clm_ctx* c, Tower& T, const void* pix, int layout, int B, void* out, int out_dtype,
-                       int normalize, hipStream_t st) {
+// image tower up to the first layer: patchify -> patch GEMM (+pos) -> class rows -> pre-LN + LN1 -> T.X
+int image_prologue(clm_ctx* c, Tower& T, const void* pix, int layout, int B, hipStream_t st) {
   const clm_model_desc& d = c->desc;
   const bool bf = c->bf16(T.vision);
   const int G = d.image_size / d.patch, Tn = G * G + 1;
@@ -705,17 +828,34 @@ int encode_image_chunk(clm_ctx* c, Tower& T, const void* pix, int layout, int B,
   LnArgs a = ln_into_x(c, T, (int64_t)B * Tn, T.pre_g, T.pre_b, T.layers[0].a_qkv, T.layers[0].r_qkv);
   a.g2 = T.layers[0].ln1_g; a.b2 = T.layers[0].ln1_b;  // pre_layrnorm (in place) then layer-0 LN1
   { PROF(CLM_PROF_LN, (double)B * Tn * T.d * 10.0); KCHK(layernorm(bf, a, st)); }
-  bool pooled_rows = false;
-  int r = run_layers(c, T, B, Tn, false, nullptr, &pooled_rows, st);
-  if (r) return r;
-  { PROF(CLM_PROF_OTHER, (double)B * (T.d * 4.0 + d.proj_dim * 4.0) + (double)T.d * d.proj_dim * 4.0);
-    KCHK(pool_project(pooled_rows ? T.hc : T.h, T.d, B, pooled_rows ? 1 : Tn, T.d, nullptr, d.eos_token_id, T.fin_g, T.fin_b, d.ln_eps, T.projT,
-                      d.proj_dim, T.pooled, out, out_dtype == CLM_F32 ? 0 : 1, normalize, st)); }
   return CLM_OK;
 }
 
-int encode_text_chunk(clm_ctx* c, Tower& T, const int32_t* ids_dev, int B, int L, void* out, int out_dtype,
-                      int normalize, hipStream_t st) {
+// pooled class rows -> post-LN -> projection (-> L2 norm) -> out
+int image_epilogue(clm_ctx* c, Tower& T, int B, bool pooled_rows, void* out, int out_dtype, int normalize,
+                   hipStream_t st) {
+  const clm_model_desc& d = c->desc;
+  const int G = d.image_size / d.patch, Tn = G * G + 1;
+  PROF(CLM_PROF_OTHER, (double)B * (T.d * 4.0 + d.proj_dim * 4.0) + (double)T.d * d.proj_dim * 4.0);
+  KCHK(pool_project(pooled_rows ? T.hc : T.h, T.d, B, pooled_rows ? 1 : Tn, T.d, nullptr, d.eos_token_id, T.fin_g,
+                    T.fin_b, d.ln_eps, T.projT, d.proj_dim, T.pooled, out, out_dtype == CLM_F32 ? 0 : 1, normalize,
+                    st));
+  return CLM_OK;
+}
+
+int encode_image_chunk(clm_ctx* c, Tower& T, const void* pix, int layout, int B, void* out, int out_dtype,
+                       int normalize, hipStream_t st) {
+  const int G = c->desc.image_size / c->desc.patch;
+  int r = image_prologue(c, T, pix, layout, B, st);
+  bool pooled_rows = false;
+  if (!r) r = run_layers(c, T, B, G * G + 1, false, nullptr, &pooled_rows, st);
+  if (!r) r = image_epilogue(c, T, B, pooled_rows, out, out_dtype, normalize, st);
+  return r;
+}
+
+// text tower up to the first layer: varlen plan (text_plan) -> token + position gather -> LN1 -> T.X.
+// *vl: whether the live rows are packed (varlen path)
+int text_prologue(clm_ctx* c, Tower& T, const int32_t* ids_dev, int B, int L, bool* vl_out, hipStream_t st) {
   const clm_model_desc& d = c->desc;
   const bool bf = c->bf16(T.vision);
   LnArgs a{};
@@ -732,16 +872,29 @@ int encode_text_chunk(clm_ctx* c, Tower& T, const int32_t* ids_dev, int B, int L
     a.m_dev = T.vl_counts;
     a.rowmap = T.vl_rowmap;
   }
+  *vl_out = vl;
   { PROF(CLM_PROF_LN, (double)B * L * T.d * 14.0); KCHK(layernorm(bf, a, st)); }
-  bool pooled_rows = false;
-  int r = run_layers(c, T, B, L, true, ids_dev, &pooled_rows, st, vl);
-  if (r) return r;
-  { PROF(CLM_PROF_OTHER, (double)B * (T.d * 4.0 + d.proj_dim * 4.0 + L * 4.0) + (double)T.d * d.proj_dim * 4.0);
-    KCHK(pool_project(pooled_rows ? T.hc : T.h, T.d, B, pooled_rows ? 1 : L, T.d, pooled_rows ? nullptr : ids_dev,
-                      d.eos_token_id, T.fin_g, T.fin_b, d.ln_eps, T.projT,
-                      d.proj_dim, T.pooled, out, out_dtype == CLM_F32 ? 0 : 1, normalize, st,
-                      vl && !pooled_rows ? T.vl_offs : nullptr)); }
   return CLM_OK;
+}
+
+// pooled first-EOS rows -> final LN -> projection (-> L2 norm) -> out
+int text_epilogue(clm_ctx* c, Tower& T, const int32_t* ids_dev, int B, int L, bool vl, bool pooled_rows, void* out,
+                  int out_dtype, int normalize, hipStream_t st) {
+  const clm_model_desc& d = c->desc;
+  PROF(CLM_PROF_OTHER, (double)B * (T.d * 4.0 + d.proj_dim * 4.0 + L * 4.0) + (double)T.d * d.proj_dim * 4.0);
+  KCHK(pool_project(pooled_rows ? T.hc : T.h, T.d, B, pooled_rows ? 1 : L, T.d, pooled_rows ? nullptr : ids_dev,
+                    d.eos_token_id, T.fin_g, T.fin_b, d.ln_eps, T.projT, d.proj_dim, T.pooled, out,
+                    out_dtype == CLM_F32 ? 0 : 1, normalize, st, vl && !pooled_rows ? T.vl_offs : nullptr));
+  return CLM_OK;
+}
+
+int encode_text_chunk(clm_ctx* c, Tower& T, const int32_t* ids_dev, int B, int L, void* out, int out_dtype,
+                      int normalize, hipStream_t st) {
+  bool vl = false, pooled_rows = false;
+  int r = text_prologue(c, T, ids_dev, B, L, &vl, st);
+  if (!r) r = run_layers(c, T, B, L, true, ids_dev, &pooled_rows, st, vl);
+  if (!r) r = text_epilogue(c, T, ids_dev, B, L, vl, pooled_rows, out, out_dtype, normalize, st);
+  return r;
 }
 
 size_t dtype_size(int dt) {
@@ -1024,10 +1177,16 @@ int clm_encode_text(clm_ctx* ctx, const int32_t* ids, int n, int L, void* out, i
 // Sub-batch launches of one encode_pair on ps[0..2*split): images on ps[2j], captions on
 // ps[2j+1]. `fork` has been recorded on ps[0]; every other stream waits on it, and ps[0]
 // waits on every other stream's pev at the end (join).
+// whether clm_encode_pair runs the grouped layers (run_layers_pair) for these arguments
+static bool pair_uses_grouped(const clm_ctx* c, int split, int n_img, int n_txt) {
+  return split == 1 && n_img > 0 && n_txt > 0 && pair_grouped() && c->vis.L == c->txt.L && c->vis.L > 0 &&
+         c->bf16(true) >= c->bf16(false);
+}
+
 static int pair_launch(clm_ctx* c, int split, hipEvent_t fork, const void* pixels, int layout, int n_img,
                        const int32_t* ids, int n_txt, int L, void* oi, void* ot, int out_dtype, int normalize) {
   const clm_model_desc& d = c->desc;
-  const int G = d.image_size / d.patch, Tn = G * G + 1;
+  const int Tn = d.image_size / d.patch * (d.image_size / d.patch) + 1;
   const size_t pix_bytes = (size_t)d.image_size * d.image_size * d.channels * (layout == CLM_PIX_U8_HWC ? 1 : 4);
   const size_t out_row = (size_t)d.proj_dim * dtype_size(out_dtype);
   for (int i = 1; i < 2 * split; ++i) HIPCHK(hipStreamWaitEvent(c->ps[i], fork, 0));
@@ -1035,6 +1194,34 @@ static int pair_launch(clm_ctx* c, int split, hipEvent_t fork, const void* pixel
     explicit Concurrent(bool on) { gemm_set_concurrent(on); }
     ~Concurrent() { gemm_set_concurrent(false); }
   } conc(n_img > 0 && n_txt > 0);
+  const int G = d.image_size / d.patch;
+  if (pair_uses_grouped(c, split, n_img, n_txt)) {
+    // grouped: the two prologues on their own streams, then every layer's ops as one launch per
+    // op on ps[0], then each tower's pruned last-layer tail + pooling on its own stream again
+    Tower& V = c->vis;
+    Tower& X = c->txt;
+    hipStream_t sv = c->ps[0], sx = c->ps[1];
+    bool vl = false;
+    int r = image_prologue(c, V, pixels, layout, n_img, sv);
+    if (!r) r = text_prologue(c, X, ids, n_txt, L, &vl, sx);
+    if (r) return r;
+    HIPCHK(hipEventRecord(c->pev[1], sx));
+    HIPCHK(hipStreamWaitEvent(sv, c->pev[1], 0));
+    LayerRun RV, RX;
+    if ((r = make_run(c, V, n_img, G * G + 1, false, nullptr, false, sv, &RV))) return r;
+    if ((r = make_run(c, X, n_txt, L, true, ids, vl, sv, &RX))) return r;
+    if ((r = run_layers_pair(c, RV, RX, sv))) return r;
+    HIPCHK(hipEventRecord(c->pev[0], sv));
+    HIPCHK(hipStreamWaitEvent(sx, c->pev[0], 0));
+    bool pv = false, px = false;
+    if ((r = post_attn_step(c, RV, V.L - 1, &pv, sv))) return r;
+    if ((r = image_epilogue(c, V, n_img, pv, oi, out_dtype, normalize, sv))) return r;
+    if ((r = post_attn_step(c, RX, X.L - 1, &px, sx))) return r;
+    if ((r = text_epilogue(c, X, ids, n_txt, L, vl, px, ot, out_dtype, normalize, sx))) return r;
+    HIPCHK(hipEventRecord(c->pev[1], sx));
+    HIPCHK(hipStreamWaitEvent(c->ps[0], c->pev[1], 0));
+    return CLM_OK;
+  }
   for (int j = 0; j < split; ++j) {
     const int i0 = (int)((int64_t)n_img * j / split), i1 = (int)((int64_t)n_img * (j + 1) / split);
     const int t0 = (int)((int64_t)n_txt * j / split), t1 = (int)((int64_t)n_txt * (j + 1) / split);
@@ -1057,6 +1244,8 @@ static int pair_launch(clm_ctx* c, int split, hipEvent_t fork, const void* pixel
   }
   return CLM_OK;
 }
+
+int clm_pair_path(const clm_ctx* ctx) { return ctx ? ctx->last_pair_path : -1; }
 
 int clm_encode_pair(clm_ctx* ctx, const void* pixels, int pix_layout, int n_img, const int32_t* ids, int n_txt,
                     int L, void* out_img, void* out_txt, int out_dtype, int normalize, int flags, void* stream) {
@@ -1090,6 +1279,7 @@ int clm_encode_pair(clm_ctx* ctx, const void* pixels, int pix_layout, int n_img,
   if (!split) split = env_split > 0 ? env_split : 1;
   split = std::max(1, std::min({split, clm_ctx::MAX_SPLIT, std::max(n_img, n_txt)}));
   const bool use_graph = (flags & CLM_PAIR_GRAPH) && !ctx->prof;
+  ctx->last_pair_path = pair_uses_grouped(ctx, split, n_img, n_txt) ? 1 : 0;
   HIPCHK(hipEventRecord(ctx->ev_fork, st));
   HIPCHK(hipStreamWaitEvent(ctx->ps[0], ctx->ev_fork, 0));
   if (!use_graph) {
@@ -1662,7 +1852,11 @@ static int search_bounded(clm_index* x, bool sampled, int64_t S, const u16* q16,
     gf.cnt = cnt; gf.cand_s = cs; gf.cand_i = ci; gf.cap = CAND_CAP; gf.base = x->offset;
     gf.m_fastest = 1;
     gf.cbound = inv_keys_of(x, st);
-    gf.debug = g_gemm_debug & 3;   // diagnostics only ($CLM_GEMM_DEBUG): main loop alone / stores dropped
+    // never clm_debug_set / $CLM_GEMM_DEBUG (those drop epilogues: the candidate lists would be
+    // empty and the top-k wrong); the filter pass's own timing knob is $CLM_SEARCH_EPI_DEBUG,
+    // read by tools only, whose results are discarded
+    static const int search_dbg = getenv("CLM_SEARCH_EPI_DEBUG") ? (atoi(getenv("CLM_SEARCH_EPI_DEBUG")) & 3) : 0;
+    gf.debug = search_dbg;
     static const bool cfg_forced = getenv("CLM_GEMM_CFG") != nullptr;
     KCHK(gemm_cfg(false, EPI_FILTER, x->dense_hits && !cfg_forced ? 1 : -1, gf, st));
     KCHK(rescore_select(cs, ci, cnt, CAND_CAP, q32 + q0 * dim, qn + q0, dim, xrows, !x->rows32, x->offset,

@@ -16,12 +16,12 @@ namespace gemm_detail {
 constexpr int GM = 4;
 constexpr int BK = 64;
 
-// Persistent tile walk of workgroup blockIdx.x over `ntiles` tiles with G workgroups: workgroup xb
+// Persistent tile walk of workgroup bid (of G) over `ntiles` tiles with G workgroups: workgroup xb
 // (the bijective XCD remap) takes tiles xb, xb + G, ... (a banded walk, one band of the tile order
 // per XCD group, left the L2 hit rate and the pair step unchanged: profiles/r02_v6_gemm_band_ab.txt)
 struct TileWalk { int first, stride, count; };
-__device__ __forceinline__ TileWalk tile_walk(int ntiles, int G) {
-  const int xb = xcd_remap(blockIdx.x, G);
+__device__ __forceinline__ TileWalk tile_walk(int ntiles, int bid, int G) {
+  const int xb = xcd_remap(bid, G);
   return TileWalk{xb, G, xb < ntiles ? (ntiles - 1 - xb) / G + 1 : 0};
 }
 
@@ -389,4 +389,6 @@ constexpr int epi_min_stores() {
 
 // G2 kernels (k_gemm2.hip): configs 8-11
 hipError_t gemm2_launch(bool bf16, int epi, int id, const GemmArgs& g, hipStream_t s);
+hipError_t gemm2_pair_launch(bool bf0, bool bf1, int epi, int id, const GemmArgs& g0, const GemmArgs& g1,
+                             const PairGrid& pg, hipStream_t s);
 }  // namespace clm

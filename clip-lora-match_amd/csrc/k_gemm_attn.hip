@@ -62,8 +62,9 @@ struct FaArgs {
   const int* lens; const int* offs; const int* tiles; const int* counts;
 };
 
+// workgroup `bid` of the `nwg` that serve one problem (gemm_attn_kernel: the whole grid)
 template <bool BF, bool CAUSAL, bool VL>
-__global__ __launch_bounds__(FA_NW * 64, 2) void gemm_attn_kernel(FaArgs a) {
+__device__ __forceinline__ void gemm_attn_body(const FaArgs& a, int bid, int nwg) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -72,15 +73,15 @@ __global__ __launch_bounds__(FA_NW * 64, 2) void gemm_attn_kernel(FaArgs a) {
   int64_t m0, M;
   if constexpr (VL) {   // grid sized for the worst case: only the live tiles run
     const int live = __builtin_amdgcn_readfirstlane(a.counts[1]) * a.H;
-    if ((int)blockIdx.x >= live) return;
-    t = xcd_remap(blockIdx.x, live);
+    if (bid >= live) return;
+    t = xcd_remap(bid, live);
     const int tw = __builtin_amdgcn_readfirstlane(a.tiles[t / a.H]);
     s0 = tw & 0xFFFF;
     nseq = tw >> 16;
     m0 = __builtin_amdgcn_readfirstlane(a.offs[s0]);
     M = __builtin_amdgcn_readfirstlane(a.counts[0]);
   } else {
-    t = xcd_remap(blockIdx.x, gridDim.x);
+    t = xcd_remap(bid, nwg);
     s0 = (t / a.H) * a.G;
     nseq = min(a.G, a.B - s0);
     m0 = (int64_t)s0 * a.T;
@@ -274,6 +275,39 @@ __global__ __launch_bounds__(FA_NW * 64, 2) void gemm_attn_kernel(FaArgs a) {
 }
 
 template <bool BF, bool CAUSAL, bool VL>
+__global__ __launch_bounds__(FA_NW * 64, 2) void gemm_attn_kernel(FaArgs a) {
+  gemm_attn_body<BF, CAUSAL, VL>(a, blockIdx.x, gridDim.x);
+}
+
+// the two towers' layer-l q/k/v + attention in one launch: workgroups [0, n0p) serve a0 (the
+// image tower: non-causal, fixed length; n0p = its tile count rounded up to a multiple of 8, the
+// padding exits), [n0p, n0p + n1) serve a1 (the causal text tower, varlen or not). One tile per
+// workgroup, the larger image tiles first: the dispatcher fills the slots the image tiles free
+// with caption tiles, so the two launches' partial last rounds become one.
+template <bool BF0, bool BF1, bool VL1>
+__global__ __launch_bounds__(FA_NW * 64, 2) void gemm_attn_pair_kernel(FaArgs a0, FaArgs a1, int n0, int n0p, int n1) {
+  const int b = blockIdx.x;
+  if (b < n0) gemm_attn_body<BF0, false, false>(a0, b, n0);
+  else if (b >= n0p) gemm_attn_body<BF1, true, VL1>(a1, b - n0p, n1);
+}
+
+template <bool BF0, bool BF1, bool VL1>
+hipError_t launch_pair(const FaArgs& a0, int n0, const FaArgs& a1, int n1, hipStream_t s) {
+  auto kern = gemm_attn_pair_kernel<BF0, BF1, VL1>;
+  static unsigned dev_done = 0;
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  if (!(__atomic_load_n(&dev_done, __ATOMIC_ACQUIRE) & (1u << (dev & 31)))) {
+    hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, FA_LDS);
+    if (e != hipSuccess) return e;
+    __atomic_fetch_or(&dev_done, 1u << (dev & 31), __ATOMIC_RELEASE);
+  }
+  const int n0p = (n0 + 7) / 8 * 8;
+  kern<<<dim3(n0p + n1), dim3(FA_NW * 64), FA_LDS, s>>>(a0, a1, n0, n0p, n1);
+  return hipGetLastError();
+}
+
+template <bool BF, bool CAUSAL, bool VL>
 hipError_t launch(const FaArgs& a, int tiles, hipStream_t s) {
   auto kern = gemm_attn_kernel<BF, CAUSAL, VL>;
   static unsigned dev_done = 0;   // >64 KiB dynamic LDS needs the opt-in attribute, once per device
@@ -293,38 +327,73 @@ bool gemm_attn_supported(int T, int H, int d, int K) {
   return T >= 1 && T <= 128 && d == H * 64 && K > 0 && K % BK == 0;
 }
 
+namespace {
+// FaArgs + workgroup count of a fixed-length launch; false if the shapes are unsupported
+bool fixed_args(const AttnProblem& p, FaArgs& a, int& grid) {
+  if (!gemm_attn_supported(p.T, p.H, p.d, p.K) || (p.ldx % 8) || (p.ldw % 8) || (p.ldo % 4) || p.ldx < p.K ||
+      p.ldw < p.K || p.ldo < p.d)
+    return false;
+  a = FaArgs{};
+  a.X = p.X; a.ldx = p.ldx; a.W = p.W; a.ldw = p.ldw; a.bias = p.bias; a.out = p.out; a.ldo = p.ldo;
+  a.B = p.B; a.T = p.T; a.H = p.H; a.d = p.d; a.K = p.K; a.G = FA_BM / p.T;
+  const int64_t tiles = (int64_t)((p.B + a.G - 1) / a.G) * p.H;
+  if (tiles > 0x7FFFFFFF) return false;
+  grid = (int)tiles;
+  return true;
+}
+// ... of a varlen launch (packed sequences; grid sized for the worst case)
+bool varlen_args(const AttnProblem& p, FaArgs& a, int& grid) {
+  if (!gemm_attn_supported(p.T, p.H, p.d, p.K) || p.B > 0xFFFF || (p.ldx % 8) || (p.ldw % 8) || (p.ldo % 4) ||
+      p.ldx < p.K || p.ldw < p.K || p.ldo < p.d || !p.lens || !p.offs || !p.tiles || !p.counts)
+    return false;
+  a = FaArgs{};
+  a.X = p.X; a.ldx = p.ldx; a.W = p.W; a.ldw = p.ldw; a.bias = p.bias; a.out = p.out; a.ldo = p.ldo;
+  a.B = p.B; a.T = p.T; a.H = p.H; a.d = p.d; a.K = p.K; a.G = 0;
+  a.lens = p.lens; a.offs = p.offs; a.tiles = p.tiles; a.counts = p.counts;
+  // text_plan closes a tile only when the next sequence does not fit, so every tile but the last
+  // holds more than 256 - L rows: at most ceil(rows / (257 - L)) + 1 tiles, and at most B
+  const int64_t max_tiles = std::min<int64_t>(p.B, ((int64_t)p.B * p.T + (256 - p.T)) / (257 - p.T) + 1);
+  const int64_t g = max_tiles * p.H;
+  if (g > 0x7FFFFFFF) return false;
+  grid = (int)g;
+  return true;
+}
+}  // namespace
+
 hipError_t gemm_attn(bool bf16, bool causal, const u16* X, int64_t ldx, const u16* W, int64_t ldw, const float* bias,
                      u16* out, int64_t ldo, int B, int T, int H, int d, int K, hipStream_t s) {
   if (B <= 0) return hipSuccess;
-  if (!gemm_attn_supported(T, H, d, K) || (ldx % 8) || (ldw % 8) || (ldo % 4) || ldx < K || ldw < K || ldo < d)
-    return hipErrorInvalidValue;
-  FaArgs a{};
-  a.X = X; a.ldx = ldx; a.W = W; a.ldw = ldw; a.bias = bias; a.out = out; a.ldo = ldo;
-  a.B = B; a.T = T; a.H = H; a.d = d; a.K = K; a.G = FA_BM / T;
-  const int64_t tiles = (int64_t)((B + a.G - 1) / a.G) * H;
-  if (tiles > 0x7FFFFFFF) return hipErrorInvalidValue;
-  if (bf16) return causal ? launch<true, true, false>(a, (int)tiles, s) : launch<true, false, false>(a, (int)tiles, s);
-  return causal ? launch<false, true, false>(a, (int)tiles, s) : launch<false, false, false>(a, (int)tiles, s);
+  AttnProblem p{X, ldx, W, ldw, bias, out, ldo, B, T, H, d, K, nullptr, nullptr, nullptr, nullptr};
+  FaArgs a;
+  int tiles;
+  if (!fixed_args(p, a, tiles)) return hipErrorInvalidValue;
+  if (bf16) return causal ? launch<true, true, false>(a, tiles, s) : launch<true, false, false>(a, tiles, s);
+  return causal ? launch<false, true, false>(a, tiles, s) : launch<false, false, false>(a, tiles, s);
 }
 
 hipError_t gemm_attn_varlen(bool bf16, bool causal, const u16* X, int64_t ldx, const u16* W, int64_t ldw,
                             const float* bias, u16* out, int64_t ldo, int B, int L, int H, int d, int K,
                             const int* lens, const int* offs, const int* tiles, const int* counts, hipStream_t s) {
   if (B <= 0) return hipSuccess;
-  if (!gemm_attn_supported(L, H, d, K) || B > 0xFFFF || (ldx % 8) || (ldw % 8) || (ldo % 4) || ldx < K || ldw < K ||
-      ldo < d || !lens || !offs || !tiles || !counts)
+  AttnProblem p{X, ldx, W, ldw, bias, out, ldo, B, L, H, d, K, lens, offs, tiles, counts};
+  FaArgs a;
+  int grid;
+  if (!varlen_args(p, a, grid)) return hipErrorInvalidValue;
+  if (bf16) return causal ? launch<true, true, true>(a, grid, s) : launch<true, false, true>(a, grid, s);
+  return causal ? launch<false, true, true>(a, grid, s) : launch<false, false, true>(a, grid, s);
+}
+
+hipError_t gemm_attn_pair(bool bf0, bool bf1, const AttnProblem& img, const AttnProblem& txt, hipStream_t s) {
+  if (img.B <= 0 || txt.B <= 0) return hipErrorInvalidValue;
+  FaArgs a0, a1;
+  int n0, n1;
+  const bool vl = txt.lens != nullptr;
+  if (!fixed_args(img, a0, n0) || !(vl ? varlen_args(txt, a1, n1) : fixed_args(txt, a1, n1)))
     return hipErrorInvalidValue;
-  FaArgs a{};
-  a.X = X; a.ldx = ldx; a.W = W; a.ldw = ldw; a.bias = bias; a.out = out; a.ldo = ldo;
-  a.B = B; a.T = L; a.H = H; a.d = d; a.K = K; a.G = 0;
-  a.lens = lens; a.offs = offs; a.tiles = tiles; a.counts = counts;
-  // text_plan closes a tile only when the next sequence does not fit, so every tile but the last
-  // holds more than 256 - L rows: at most ceil(rows / (257 - L)) + 1 tiles, and at most B
-  const int64_t max_tiles = std::min<int64_t>(B, ((int64_t)B * L + (256 - L)) / (257 - L) + 1);
-  const int64_t grid = max_tiles * H;
-  if (grid > 0x7FFFFFFF) return hipErrorInvalidValue;
-  if (bf16) return causal ? launch<true, true, true>(a, (int)grid, s) : launch<true, false, true>(a, (int)grid, s);
-  return causal ? launch<false, true, true>(a, (int)grid, s) : launch<false, false, true>(a, (int)grid, s);
+  if (bf0 && !bf1) return vl ? launch_pair<true, false, true>(a0, n0, a1, n1, s) : launch_pair<true, false, false>(a0, n0, a1, n1, s);
+  if (bf0 && bf1) return vl ? launch_pair<true, true, true>(a0, n0, a1, n1, s) : launch_pair<true, true, false>(a0, n0, a1, n1, s);
+  if (!bf0 && !bf1) return vl ? launch_pair<false, false, true>(a0, n0, a1, n1, s) : launch_pair<false, false, false>(a0, n0, a1, n1, s);
+  return hipErrorInvalidValue;
 }
 
 }  // namespace clm

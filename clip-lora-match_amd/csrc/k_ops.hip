@@ -106,14 +106,14 @@ __global__ __launch_bounds__(256) void ln_kernel(LnArgs aa) {
 // d % 256 == 0: lane owns NQ float4 at e = (i*64 + lane)*4 (16-B loads, 8-B bf16 stores: half
 // the memory instructions of the float2 form above; HBM-bound).
 template <bool BF, int NQ, int R = 2>
-__global__ __launch_bounds__(256) void ln4_kernel(LnArgs aa) {
+__device__ __forceinline__ void ln4_body(const LnArgs& aa, int bid) {
   LnArgs a = aa;   // varlen: the device-resident row count (the grid was sized for aa.M)
   if (a.m_dev) a.M = __builtin_amdgcn_readfirstlane(*a.m_dev);
   // R rows per wave (every row's loads issued before any is reduced; gamma / beta loaded
   // once per wave and reused); the 16-B paired store path below takes rows in pairs
   static_assert(R % 2 == 0, "rows per wave come in pairs");
   const int lane = threadIdx.x & 63;
-  const int row0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * R;
+  const int row0 = (bid * 4 + (threadIdx.x >> 6)) * R;
   if (row0 >= a.M) return;
   constexpr int d = NQ * 256;
   float4 x[R][NQ];
@@ -228,6 +228,31 @@ __global__ __launch_bounds__(256) void ln4_kernel(LnArgs aa) {
       if (lane < a.r_pad) y[d + lane] = from_f32<BF>(lane < a.r_ext ? mine : 0.f);
     }
   }
+}
+
+template <bool BF, int NQ, int R = 2>
+__global__ __launch_bounds__(256) void ln4_kernel(LnArgs a) {
+  ln4_body<BF, NQ, R>(a, blockIdx.x);
+}
+
+// the two towers' LayerNorms of one layer in one launch: blocks [0, nb0) normalise a0's rows
+// (image tower, d = 256 NQ0), the rest a1's (text tower, d = 256 NQ1); each row exactly as
+// ln4_kernel computes it
+template <bool BF0, int NQ0, bool BF1, int NQ1>
+__global__ __launch_bounds__(256) void ln4_pair_kernel(LnArgs a0, LnArgs a1, int nb0) {
+  const int b = blockIdx.x;
+  if (b < nb0) ln4_body<BF0, NQ0>(a0, b);
+  else ln4_body<BF1, NQ1>(a1, b - nb0);
+}
+
+template <bool BF0, bool BF1>
+hipError_t ln_pair_dims(const LnArgs& a0, const LnArgs& a1, hipStream_t s) {
+  const int nb0 = (a0.M + 7) / 8, nb1 = (a1.M + 7) / 8;
+  if (a0.d == 768 && a1.d == 512) ln4_pair_kernel<BF0, 3, BF1, 2><<<nb0 + nb1, 256, 0, s>>>(a0, a1, nb0);
+  else if (a0.d == 1024 && a1.d == 768) ln4_pair_kernel<BF0, 4, BF1, 3><<<nb0 + nb1, 256, 0, s>>>(a0, a1, nb0);
+  else if (a0.d == 512 && a1.d == 512) ln4_pair_kernel<BF0, 2, BF1, 2><<<nb0 + nb1, 256, 0, s>>>(a0, a1, nb0);
+  else return hipErrorNotSupported;
+  return hipGetLastError();
 }
 
 template <bool BF>
@@ -676,6 +701,19 @@ hipError_t layernorm(bool bf16, const LnArgs& a, hipStream_t s) {
   if (a.M <= 0) return hipSuccess;
   if (a.r_ext > 64 || a.r_pad > 64) return hipErrorInvalidValue;
   return bf16 ? ln_dispatch<true>(a, s) : ln_dispatch<false>(a, s);
+}
+
+hipError_t layernorm_pair(bool bf0, bool bf1, const LnArgs& a0, const LnArgs& a1, hipStream_t s) {
+  if (a0.M <= 0) return layernorm(bf1, a1, s);
+  if (a1.M <= 0) return layernorm(bf0, a0, s);
+  if (a0.r_ext > 64 || a0.r_pad > 64 || a1.r_ext > 64 || a1.r_pad > 64) return hipErrorInvalidValue;
+  hipError_t e = hipErrorNotSupported;
+  if (bf0 && !bf1) e = ln_pair_dims<true, false>(a0, a1, s);
+  else if (bf0 && bf1) e = ln_pair_dims<true, true>(a0, a1, s);
+  else if (!bf0 && !bf1) e = ln_pair_dims<false, false>(a0, a1, s);
+  if (e != hipErrorNotSupported) return e;
+  e = layernorm(bf0, a0, s);   // other widths: two launches
+  return e != hipSuccess ? e : layernorm(bf1, a1, s);
 }
 
 hipError_t lora_down(bool bf16, u16* X, int64_t ldx, int M, int K, const float* A, int r_ext, int r_pad,

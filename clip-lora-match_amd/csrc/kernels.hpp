@@ -61,6 +61,20 @@ int gemm_num_configs();
 // other stream; alone, the slot-filling 160x128 tiles are faster (profiles/r02_v4_gemm_160x128.txt)
 void gemm_set_concurrent(bool on);
 
+// Grouped launch of two independent GEMMs with one epilogue (EPI_RESID or EPI_GELU): the two
+// CLIP towers' layer-l out_proj / fc1 / fc2 (clm_encode_pair, grouped mode). Workgroups [0, G0)
+// run g0 (operand type bf0), [n0, n0 + G1) run g1 (bf1); each range walks its own problem's tiles
+// exactly as gemm() would, so every output bit equals the separate launches'. (bf0, bf1) =
+// (bf16, fp16) is the mixed assignment; (fp16, bf16) is not instantiated. No split-K.
+struct PairGrid { int G0, n0, G1; };
+// config < 0: pick_pair_config; persist: 0 = one tile per workgroup (the dispatcher balances the
+// two problems' tiles over the slots), 1 = persistent ranges splitting the slots by work
+hipError_t gemm_pair(bool bf0, bool bf1, int epi, int config, const GemmArgs& g0, const GemmArgs& g1, int persist,
+                     hipStream_t s);
+// tile configuration of a grouped launch: greedy list-scheduling makespan of both problems' tiles
+// over the config's slots (tiles in launch order, per-tile cost BM * BN * K / efficiency)
+int pick_pair_config(int epi, const GemmArgs& g0, const GemmArgs& g1);
+
 // ----------------------------------------------------------- row ops -------
 // LayerNorm over rows of a fp32 matrix, one wave per row.
 //   mode 0: x = src rows                         (src = h)
@@ -84,6 +98,9 @@ struct LnArgs {
   const int* m_dev; const int* rowmap;
 };
 hipError_t layernorm(bool bf16, const LnArgs& a, hipStream_t s);
+// the image and text towers' LayerNorms of one layer in one launch (d0 / d1 = 768 / 512 or
+// 1024 / 768; other widths run as two launches), rows bit-identical to layernorm()
+hipError_t layernorm_pair(bool bf0, bool bf1, const LnArgs& a0, const LnArgs& a1, hipStream_t s);
 
 // y[:, K : K+r_pad) = (X[:, :K] . A^T) for LoRA K-extension of a GEMM whose input
 // is not a LayerNorm output (out_proj after attention, fc2 after GELU).
@@ -152,6 +169,15 @@ hipError_t gemm_attn(bool bf16, bool causal, const u16* X, int64_t ldx, const u1
 hipError_t gemm_attn_varlen(bool bf16, bool causal, const u16* X, int64_t ldx, const u16* W, int64_t ldw,
                             const float* bias, u16* out, int64_t ldo, int B, int L, int H, int d, int K,
                             const int* lens, const int* offs, const int* tiles, const int* counts, hipStream_t s);
+// one problem of a grouped (two-tower) fused q/k/v + attention launch; lens == null: fixed length T
+struct AttnProblem {
+  const u16* X; int64_t ldx; const u16* W; int64_t ldw; const float* bias; u16* out; int64_t ldo;
+  int B, T, H, d, K;
+  const int *lens, *offs, *tiles, *counts;   // varlen (text_plan) or null
+};
+// image tower (non-causal, fixed T) + text tower (causal; varlen if txt.lens) in one launch,
+// bit-identical to gemm_attn / gemm_attn_varlen of each; (bf0, bf1) != (fp16, bf16)
+hipError_t gemm_attn_pair(bool bf0, bool bf1, const AttnProblem& img, const AttnProblem& txt, hipStream_t s);
 
 // ----------------------------------------------------------- search --------
 // rows f32|f16 [n, dim] -> fp16 dst + fp32 inverse norms of the fp16-rounded rows

@@ -170,6 +170,11 @@ class ClipLoraModel:
                 "clm_encode_pair")
         return oi, ot
 
+    def pair_path(self) -> str:
+        """how the last encode_pair ran: "grouped" (one launch per op for both towers' layer),
+        "streams" (a stream per tower piece) or "none"."""
+        return {1: "grouped", 0: "streams"}.get(C.lib().clm_pair_path(self._ctx), "none")
+
     # ------------------------------------------------------------ timing --
     def prof_enable(self, enable: bool = True) -> None:
         C.check(C.lib().clm_prof_enable(self._ctx, int(bool(enable))), "clm_prof_enable")

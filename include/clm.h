@@ -147,6 +147,10 @@ enum { CLM_PAIR_GRAPH = 1, CLM_PAIR_SPLIT_SHIFT = 8 };
 int clm_encode_pair(clm_ctx* ctx, const void* pixels, int pix_layout, int n_img, const int32_t* ids,
                     int n_txt, int L, void* out_img, void* out_txt, int out_dtype, int normalize,
                     int flags, void* stream);
+/* How the last clm_encode_pair ran: 0 = one stream per tower piece (default), 1 = grouped
+ * (opt-in: env CLM_PAIR_GROUPED=1 or clm_debug_set bit 64; S = 1 and both towers with the same
+ * layer count: each layer's ops of both towers as one launch per op), -1 = no call yet. */
+int clm_pair_path(const clm_ctx* ctx);
 
 /* GPU-resident cosine index (dim % 64 == 0, <= 1024). Scores are the EXACT cosine of the
  * caller's query and rows (fp64 arithmetic, rounded once to fp32): an fp16 MFMA pass bounds the

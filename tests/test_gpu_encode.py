@@ -314,3 +314,51 @@ def test_text_varlen_bit_identical(preset, dtype):
                 assert torch.equal(a, b), f"case {i}: varlen vs padded max diff {(a - b).abs().max().item():.3e}"
     for i, (a, b) in enumerate(zip(outs[8], outs[40])):
         assert torch.equal(a, b), f"every-row case {i}: varlen vs padded"
+
+
+@pytest.mark.parametrize("preset,dtype,mode", [("tiny", "float16", "merged"), ("ViT-B/32", "float16", "merged"),
+                                               ("ViT-B/32", "mixed", "merged"), ("ViT-B/32", "bfloat16", "merged"),
+                                               ("ViT-B/32", "float16", "unmerged")])
+def test_grouped_pair_bit_identical(preset, dtype, mode):
+    """Grouped encode_pair (clm_debug_set bit 64, opt-in: each layer's attention / out_proj / LN /
+    fc1 / fc2 of BOTH towers as one launch per op, capi.cpp run_layers_pair) == the two-stream
+    default == the single-tower calls, bit for bit: ragged batch sizes (partial
+    tiles of both problems), varlen captions with ragged lengths and a caption without EOS, graph
+    replay with new contents behind the same pointers, pruned and every-row last layer (bit 8)."""
+    from clip_lora_match_amd import _capi as C
+    m, cfg, sd, lora = _model(preset, dtype, mode, max_batch=64)
+    imgs = torch.from_numpy(syn.images_u8(37, cfg.image_size, 91)).cuda()
+    ids = syn.captions(61, cfg.max_pos, cfg.bos_token_id, cfg.eos_token_id, 92, min_len=2)
+    ids[3] = np.arange(cfg.max_pos) + 5           # no EOS at all
+    ids = torch.from_numpy(ids).cuda()
+    outs = {}
+    try:
+        for flag in (0, 64, 8, 72):
+            C.lib().clm_debug_set(flag)
+            res = [m.encode_pixels(imgs), m.encode_ids(ids)]
+            for graph in (False, True):
+                oi = torch.empty_like(res[0])
+                ot = torch.empty_like(res[1])
+                for _ in range(2):
+                    m.encode_pair(imgs, ids, out_img=oi, out_txt=ot, graph=graph, split=1)
+                    torch.cuda.synchronize()
+                assert m.pair_path() == ("grouped" if flag & 64 else "streams"), (flag, m.pair_path())
+                res += [oi.clone(), ot.clone()]
+            outs[flag] = res
+        # graph replay sees new pixels behind the same pointers
+        C.lib().clm_debug_set(64)
+        imgs2 = torch.from_numpy(syn.images_u8(37, cfg.image_size, 93)).cuda()
+        imgs.copy_(imgs2)
+        oi = torch.empty_like(outs[0][0])
+        ot = torch.empty_like(outs[0][1])
+        m.encode_pair(imgs, ids, out_img=oi, out_txt=ot, graph=True, split=1)
+        torch.cuda.synchronize()
+        assert torch.equal(oi, m.encode_pixels(imgs2)) and torch.equal(ot, outs[0][1])
+    finally:
+        C.lib().clm_debug_set(0)
+    for flag in (0, 64, 8, 72):
+        r = outs[flag]
+        for i in range(2, 6):
+            assert torch.equal(r[i], r[i % 2]), (flag, i, (r[i] - r[i % 2]).abs().max().item())
+    for i in range(6):
+        assert torch.equal(outs[0][i], outs[64][i]) and torch.equal(outs[8][i], outs[72][i]), i
