@@ -808,7 +808,10 @@ def lora_unmerged_leg(cfg, sd, lora, dev, B, imgs, ids, steps, warmup, dtype):
             "ms_per_step": round(dt * 1e3, 4)}
 
 
-EXCHANGE = "fp16"   # configs[2]'s all_gather form (1.0 GB for 1 M x 512)
+# configs[2]'s all_gather form: fp32 rows as encoded (the reference's .pt content; 2.05 GB for 1 M x
+# 512 at N > 1). The fp16 exchange (half the link bytes, rows re-normalised after the
+# gather) is reported beside it as a variant: its all_gather time and how far it moves the rows.
+EXCHANGE = "fp32"
 
 
 def index_build_leg(dev, world: int, rank: int, n_images: int, batch: int, dtype: str) -> dict:
@@ -822,7 +825,7 @@ def index_build_leg(dev, world: int, rank: int, n_images: int, batch: int, dtype
     import shutil
     import tempfile
     from clip_lora_match_amd.distributed import all_gather_rows, shard_range
-    from clip_lora_match_amd.index_build import _save_index, encode_items, fold_sha256
+    from clip_lora_match_amd.index_build import _f16_exchange, _f16_restore, _save_index, encode_items, fold_sha256
     from clip_lora_match_amd.processor import ClipProcessor
     cfg = clm.get_preset("ViT-B/32")
     m = ClipLoraModel(cfg, device=dev, compute_dtype=dtype, lora_mode="merged", max_batch=batch)
@@ -859,16 +862,23 @@ def index_build_leg(dev, world: int, rank: int, n_images: int, batch: int, dtype
         sync()
         t2 = time.perf_counter()
         enc_s, total_s = max_over_ranks(t1 - t0), max_over_ranks(t2 - t0)
-        gather_ms = None
+        gather_ms = {}
         if world > 1:
             a, b = shard_range(n_images, rank, world)
-            local = rows[a:b].to(torch.float16 if EXCHANGE == "fp16" else torch.float32).contiguous()
-            sync()
-            tg = time.perf_counter()
-            all_gather_rows(local, n_images)
-            torch.cuda.synchronize()
-            gather_ms = round(max_over_ranks(time.perf_counter() - tg) * 1e3, 3)
+            for ex, dt in (("fp32", torch.float32), ("fp16", torch.float16)):
+                local = rows[a:b].to(dt).contiguous()
+                sync()
+                tg = time.perf_counter()
+                all_gather_rows(local, n_images)
+                torch.cuda.synchronize()
+                gather_ms[ex] = round(max_over_ranks(time.perf_counter() - tg) * 1e3, 3)
         sha = fold_sha256(rows)   # checksum of checksums of every row's bits
+        # the fp16-exchange variant's rows (what every rank would keep): their distance from these
+        r16 = _f16_restore(_f16_exchange(rows))
+        f16_var = {"max_abs_component_diff": float((r16 - rows).abs().max()),
+                   "max_1_minus_cos": float((1 - (r16.double() * rows.double()).sum(1)).max()),
+                   "index_fold_sha256": fold_sha256(r16)}
+        del r16
         pt_bytes = os.path.getsize(os.path.join(tmpdir, "index.pt")) if rank == 0 else None
     finally:
         m.close()
@@ -882,12 +892,15 @@ def index_build_leg(dev, world: int, rank: int, n_images: int, batch: int, dtype
            "encode_images_per_s": round(n_images / enc_s, 1), "encode_gather_s": round(enc_s, 3),
            "write_s": round(total_s - enc_s, 3), "pt_bytes": pt_bytes,
            "tflops": round(flops / enc_s / 1e12, 1), "index_fold_sha256": sha, "exchange": EXCHANGE,
-           "note": "index_fold_sha256 is equal at every world size when the sharded build is bit-identical; "
-                   "exchange fp16: rows cross the links as fp16 and are re-normalised in fp32 after the gather, "
-                   "the same round trip at world 1 (index_build.encode_items)"}
+           "fp16_exchange_variant": f16_var,
+           "note": "index_fold_sha256 is equal at every world size when the sharded build is bit-identical "
+                   "(tests/test_gpu_distributed.py builds the same 1 M rows and prints its world-1 fold); "
+                   "fp16_exchange_variant: the same rows rounded to fp16 for the all_gather and re-normalised "
+                   "in fp32 after it (index_build exchange='fp16'), compared with the fp32 rows"}
     if world > 1:
-        out.update({"n_gpus": world, "all_gather_ms": gather_ms,
-                    "all_gather_bytes": n_images * cfg.proj_dim * (2 if EXCHANGE == "fp16" else 4),
+        out.update({"n_gpus": world, "all_gather_ms": gather_ms.get(EXCHANGE),
+                    "all_gather_ms_fp16_variant": gather_ms.get("fp16"),
+                    "all_gather_bytes": n_images * cfg.proj_dim * 4,
                     "parallelism": f"batch-sharded encode + all_gather({EXCHANGE} embeddings) over xGMI"})
     return out
 

@@ -225,11 +225,8 @@ struct clm_index {
   unsigned* inv_keys = nullptr; int64_t inv_keys_n = -1;
   // queries served by: [0] sampled bounded search, [1] the full exact scan, [2] overflow re-runs,
   // [3] bounded search with the chunked fp16 scan as step 1
-  int64_t search_stats[4] = {0, 0, 0, 0};
-  // the last bounded search had most of its candidate lists overflow (near-duplicate rows): the
-  // next one runs its filter pass on gemm_kernel's 256 x 256 tiles, whose FILTER epilogue is the
-  // faster one when appends dominate (same candidates either way)
-  bool dense_hits = false;
+  // [4] / [5]: queries whose filter pass ran on G2 256 x 192 / gemm_kernel 256 x 256 (dense blocks)
+  int64_t search_stats[6] = {0, 0, 0, 0, 0, 0};
 };
 
 namespace {
@@ -1325,8 +1322,8 @@ int clm_encode_pair(clm_ctx* ctx, const void* pixels, int pix_layout, int n_img,
 // 24-115, similarity.py:36-58). Search = an fp16 MFMA pass that bounds the candidates, then an
 // exact fp64 re-score of the candidates against the caller's own rows (see clm_index_search).
 int clm_index_create(int hip_device, int64_t capacity, int dim, clm_index** out) {
-  if (!out || capacity < 0 || dim <= 0 || dim % 64 || dim > 1024)
-    return fail(CLM_E_ARG, "bad capacity/dim (dim must be a multiple of 64, <= 1024)");
+  if (!out || capacity < 0 || dim <= 0 || dim % 64 || dim > 65536)
+    return fail(CLM_E_ARG, "bad capacity/dim (dim must be a multiple of 64, <= 65536)");
   DeviceGuard g(hip_device);
   clm_index* x = new clm_index();
   x->dev = hip_device;
@@ -1399,7 +1396,6 @@ int clm_index_append(clm_index* x, const void* rows, int dtype, int64_t n, void*
   if (r) return r;
   x->samp_n = -1;   // the threshold sample is rebuilt from the new row set
   x->inv_keys_n = -1;
-  x->dense_hits = false;
   if (dtype == CLM_F32 && !x->rows32) {
     // first fp32 rows: keep an fp32 copy from now on; the rows so far were fp16 as given
     if (hipMalloc(&x->rows32, (size_t)x->cap * x->dim * sizeof(float)) != hipSuccess) {
@@ -1477,7 +1473,6 @@ int clm_index_import(clm_index* x, const uint16_t* rows16, const float* inv, con
   if (r) return r;
   x->samp_n = -1;
   x->inv_keys_n = -1;
-  x->dense_hits = false;
   const size_t cnt = (size_t)n * x->dim;
   if (rows32 && !x->rows32) {   // as clm_index_append: the first fp32 rows start the fp32 copy
     if (hipMalloc(&x->rows32, (size_t)x->cap * x->dim * sizeof(float)) != hipSuccess) {
@@ -1507,7 +1502,6 @@ int clm_index_reset(clm_index* x) {
   x->n = 0;
   x->samp_n = -1;   // never reuse a sample of the previous rows
   x->inv_keys_n = -1;
-  x->dense_hits = false;
   return CLM_OK;
 }
 
@@ -1566,6 +1560,17 @@ struct Scratch {
   void* p = nullptr;
   size_t bytes = 0;
 };
+// A call that needed more than SCRATCH_KEEP bytes (a one-off host-staged score matrix, a resize
+// of large photos) frees its scratch once its stream has drained it, so that peak does not stay
+// allocated for the life of the process (the caller holds scr.mu)
+constexpr size_t SCRATCH_KEEP = (size_t)256 << 20;
+static void scratch_trim(Scratch& scr) {
+  if (scr.bytes <= SCRATCH_KEEP) return;
+  (void)hipFree(scr.p);
+  (void)hipGetLastError();
+  scr.p = nullptr;
+  scr.bytes = 0;
+}
 static Scratch& scratch_of_current_device() {
   static Scratch s[64];
   int d = 0;
@@ -1578,6 +1583,10 @@ static Scratch& scratch_of_current_device() {
 // products). Every row of the exact top-k therefore has an fp16-pass score within 2 x 2.05e-3 of
 // the fp16-pass k-th best; the candidates are taken that wide (plus slack) and re-scored exactly.
 constexpr float RESCORE_MARGIN = 5e-3f;
+// ... while the fp32 accumulation error stays inside the slack: dim * 2^-24 <= 4.9e-4 for dim <= 8192
+// (every score within 1.95e-3 + 4.9e-4 of the exact cosine, twice that < RESCORE_MARGIN). Wider
+// rows are always searched by the exact scan.
+constexpr int MARGIN_MAX_DIM = 8192;
 constexpr int CAND_CAP = 2048;
 
 // Chunked scan: score chunks [nqb, ch] -- fp16 MFMA (EPI_SCORE GEMM) or exact fp64 cosines
@@ -1632,6 +1641,38 @@ static int search_scan(clm_index* x, bool exact, const u16* q16, const float* qi
       }
     }
     if (nchunks > 1) KCHK(topk_merge(cs, ci, nb, (int)nchunks, k, k, osc + q0 * k, oix + q0 * k, st));
+  }
+  return CLM_OK;
+}
+
+// Exact scan for k > 1024 (torch.topk of search.py:98 / similarity.py:57 takes any k <= N): every
+// row of a query block scored exactly into one [nqb, N] matrix, then topk_any (exact k-th key,
+// collection, LDS run sort + merge passes). The block is sized so the scores and topk_any's
+// workspace stay within a 1 GiB budget (at least one query).
+static int search_scan_large(clm_index* x, const float* q32, const double* qn, int64_t nq, int k, float* osc,
+                             int64_t* oix, hipStream_t st) {
+  const int dim = (int)x->dim;
+  const int64_t N = x->n;
+  const size_t budget = (size_t)1 << 30;
+  const size_t per_q = (size_t)std::max<int64_t>(N, 1) * 4 + topk_any_ws_bytes(1, k);
+  int64_t nqb = std::max<int64_t>(1, std::min<int64_t>(nq, (int64_t)(budget / per_q)));
+  nqb = std::min<int64_t>(nqb, 65535);
+  size_t off = 0;
+  auto take = [&](size_t bytes) { size_t o = off; off = round_up(off + bytes, 256); return o; };
+  const size_t o_sc = take((size_t)nqb * std::max<int64_t>(N, 1) * 4);
+  const size_t o_ws = take(topk_any_ws_bytes(nqb, k));
+  int r = grow(&x->ws3, &x->ws3_bytes, off);
+  if (r) return r;
+  uint8_t* w = (uint8_t*)x->ws3;
+  float* sc = (float*)(w + o_sc);
+  for (int64_t q0 = 0; q0 < nq; q0 += nqb) {
+    const int64_t nb = std::min(nqb, nq - q0);
+    if (N > 0) {
+      const void* rp = x->rows32 ? (const void*)x->rows32 : (const void*)x->rows;
+      KCHK(exact_scores(q32 + q0 * dim, qn + q0, nb, rp, !x->rows32, N, dim, sc, N, st));
+    }
+    KCHK(topk_any(sc, std::max<int64_t>(N, 1), nullptr, 0, nb, N, k, x->offset, osc + q0 * k, oix + q0 * k, k,
+                  w + o_ws, st));
   }
   return CLM_OK;
 }
@@ -1811,6 +1852,7 @@ static int search_bounded(clm_index* x, bool sampled, int64_t S, const u16* q16,
   const size_t o_ti = take((size_t)nqb * k * 8);
   const size_t o_th = take((size_t)nq * 4);   // every query's threshold (the overflow pass reuses them)
   const size_t o_cnt = take((size_t)nqb * 4);
+  const size_t o_est = take((size_t)nqb * 4);
   const size_t o_cs = take((size_t)nqb * CAND_CAP * 4);
   const size_t o_ci = take((size_t)nqb * CAND_CAP * 8);
   if ((r = grow(&x->ws2, &x->ws2_bytes, off))) return r;
@@ -1820,6 +1862,8 @@ static int search_bounded(clm_index* x, bool sampled, int64_t S, const u16* q16,
   int64_t* ti = (int64_t*)(w + o_ti);
   float* th = (float*)(w + o_th);
   int* cnt = (int*)(w + o_cnt);
+  int* est = (int*)(w + o_est);
+  std::vector<int> hest;
   float* cs = (float*)(w + o_cs);
   int64_t* ci = (int64_t*)(w + o_ci);
   const void* xrows = x->rows32 ? (const void*)x->rows32 : (const void*)x->rows;
@@ -1827,6 +1871,11 @@ static int search_bounded(clm_index* x, bool sampled, int64_t S, const u16* q16,
   std::vector<int64_t> overflow, ocount;
   for (int64_t q0 = 0; q0 < nq; q0 += nqb) {
     const int64_t nb = std::min(nqb, nq - q0);
+    // Filter tile for this block, from the block's own data: when most of its queries' candidate
+    // windows hold more than CAND_CAP rows (near-duplicate rows: the sampled count above the
+    // threshold, scaled by N / S), the appends dominate the pass and gemm_kernel's 256 x 256 FILTER
+    // epilogue is the faster one; otherwise G2's 256 x 192 (same candidates either way)
+    bool dense = false;
     if (sampled) {
       GemmArgs ga{};
       ga.A = q16 + q0 * dim; ga.lda = dim; ga.W = x->samp; ga.ldw = dim;
@@ -1839,6 +1888,13 @@ static int search_bounded(clm_index* x, bool sampled, int64_t S, const u16* q16,
         KCHK(topk_rows(sc, S, nb, S, k, 0, ts, ti, k, st));
         KCHK(filter_thresholds(ts, k, nb, k, RESCORE_MARGIN, th + q0, st));
       }
+      KCHK(count_ge(sc, S, nb, S, th + q0, est, st));
+      hest.resize(nb);
+      HIPCHK(hipMemcpyAsync(hest.data(), est, (size_t)nb * 4, hipMemcpyDeviceToHost, st));
+      HIPCHK(hipStreamSynchronize(st));
+      int64_t over = 0;
+      for (int64_t i = 0; i < nb; ++i) over += (double)hest[i] * ((double)N / (double)S) > CAND_CAP;
+      dense = 2 * over > nb;
     } else {
       if ((r = search_scan(x, false, q16 + q0 * dim, qinv + q0, nullptr, nullptr, nb, k, ts, ti, st))) return r;
       KCHK(filter_thresholds(ts, k, nb, k, RESCORE_MARGIN, th + q0, st));
@@ -1858,7 +1914,8 @@ static int search_bounded(clm_index* x, bool sampled, int64_t S, const u16* q16,
     static const int search_dbg = getenv("CLM_SEARCH_EPI_DEBUG") ? (atoi(getenv("CLM_SEARCH_EPI_DEBUG")) & 3) : 0;
     gf.debug = search_dbg;
     static const bool cfg_forced = getenv("CLM_GEMM_CFG") != nullptr;
-    KCHK(gemm_cfg(false, EPI_FILTER, x->dense_hits && !cfg_forced ? 1 : -1, gf, st));
+    KCHK(gemm_cfg(false, EPI_FILTER, dense && !cfg_forced ? 1 : -1, gf, st));
+    x->search_stats[dense ? 5 : 4] += nb;
     KCHK(rescore_select(cs, ci, cnt, CAND_CAP, q32 + q0 * dim, qn + q0, dim, xrows, !x->rows32, x->offset,
                         RESCORE_MARGIN, nb, k, osc + q0 * k, oix + q0 * k, st));
     hcnt.resize(nb);
@@ -1871,7 +1928,6 @@ static int search_bounded(clm_index* x, bool sampled, int64_t S, const u16* q16,
       }
   }
   x->search_stats[sampled ? 0 : 3] += nq - (int64_t)overflow.size();
-  x->dense_hits = 2 * (int64_t)overflow.size() > nq;
   if (overflow.empty()) return CLM_OK;
   // Candidate lists beyond CAND_CAP (near-duplicate rows inside the window). Lists of up to
   // (SORT_MAX / k) chunks are rebuilt whole by a second filter pass over just those queries and
@@ -1926,7 +1982,8 @@ int clm_index_search(clm_index* x, const void* q, int q_dtype, int64_t nq, int k
                      int64_t* out_idx, void* stream) {
   if (!x || nq < 0 || (nq > 0 && (!q || !out_scores || !out_idx))) return fail(CLM_E_ARG, "bad argument");
   if (q_dtype != CLM_F32 && q_dtype != CLM_F16) return fail(CLM_E_ARG, "queries must be f32 or f16");
-  if (k < 1 || k > 1024) return fail(CLM_E_ARG, "k must be in [1, 1024]");
+  if (k < 1) return fail(CLM_E_ARG, "k must be >= 1");
+  if (k > (1 << 26)) return fail(CLM_E_ARG, "k must be <= 2^26");
   if (nq == 0) return CLM_OK;
   DeviceGuard g(x->dev);
   hipStream_t st = (hipStream_t)stream;
@@ -1971,7 +2028,12 @@ int clm_index_search(clm_index* x, const void* q, int q_dtype, int64_t nq, int k
   const char* e_exact = getenv("CLM_SEARCH_EXACT");
   const char* e_bounded = getenv("CLM_SEARCH_BOUNDED");   // tests: bounded search at any size
   const bool force_bounded = e_bounded && atoi(e_bounded) && N > 0;
-  if ((e_full && atoi(e_full)) || N == 0 || (!force_bounded && (double)nq * (double)N <= (double)(1 << 24))) {
+  if (k > 1024) {
+    // any k: the exact scan over whole rows (topk_rows / the candidate lists stop at 1024)
+    r = search_scan_large(x, q32, qn, nq, k, osc, oix, st);
+    x->search_stats[1] += nq;
+  } else if ((e_full && atoi(e_full)) || N == 0 || dim > MARGIN_MAX_DIM ||
+             (!force_bounded && (double)nq * (double)N <= (double)(1 << 24))) {
     r = search_scan(x, true, q16, qinv, q32, qn, nq, k, osc, oix, st);
     x->search_stats[1] += nq;
   } else {
@@ -2003,8 +2065,9 @@ int clm_index_stats(const clm_index* x, int64_t* filtered, int64_t* exact, int64
 
 int clm_index_stats2(const clm_index* x, int64_t* out, int n) {
   if (!x || !out || n < 0) return fail(CLM_E_ARG, "bad argument");
-  const int64_t v[4] = {x->search_stats[0], x->search_stats[3], x->search_stats[1], x->search_stats[2]};
-  for (int i = 0; i < n && i < 4; ++i) out[i] = v[i];
+  const int64_t v[6] = {x->search_stats[0], x->search_stats[3], x->search_stats[1], x->search_stats[2],
+                        x->search_stats[4], x->search_stats[5]};
+  for (int i = 0; i < n && i < 6; ++i) out[i] = v[i];
   return CLM_OK;
 }
 
@@ -2038,6 +2101,7 @@ int clm_cosine_scores(int hip_device, const float* q, int64_t nq, const float* c
   if (e == hipSuccess) e = exact_scores(qs, qn, nq, cs, false, n, dim, os, n, st);
   if (e == hipSuccess && !od) e = hipMemcpyAsync(out, os, (size_t)nq * n * 4, hipMemcpyDeviceToHost, st);
   if (e == hipSuccess) e = hipStreamSynchronize(st);
+  scratch_trim(scr);
   if (e != hipSuccess) rc = fail(CLM_E_HIP, std::string("cosine_scores: ") + hipGetErrorString(e));
   return rc;
 }
@@ -2063,14 +2127,18 @@ int clm_topk_threshold(int hip_device, const float* scores, int64_t lds, int64_t
   KCHK(topk_rows(scores, lds, nq, C, k, 0, ts, ti, k, st));
   KCHK(filter_thresholds(ts, k, nq, k, margin, th, st));
   HIPCHK(hipStreamSynchronize(st));   // the scratch is reused by the next call
+  scratch_trim(scr);
   return CLM_OK;
 }
 
 int clm_topk_merge(int hip_device, const float* scores, const int64_t* idx, int64_t nq, int parts, int k_in, int k,
                    float* out_scores, int64_t* out_idx, void* stream) {
-  if (nq < 0 || parts <= 0 || k_in <= 0 || k <= 0 || k > 1024 || (int64_t)parts * k_in > 8192)
-    return fail(CLM_E_ARG, "bad merge shape (parts*k_in <= 8192, k <= 1024)");
+  if (nq < 0 || parts <= 0 || k_in <= 0 || k <= 0 || (int64_t)parts * k_in > 0x7FFFFFFF)
+    return fail(CLM_E_ARG, "bad merge shape");
   if (nq == 0) return CLM_OK;
+  // one LDS sort per row (topk_merge) up to 8192 candidates and k <= 1024; beyond, topk_any
+  const bool any = k > 1024 || (int64_t)parts * k_in > 8192;
+  const int64_t any_rows = std::min<int64_t>(nq, 65535);
   DeviceGuard g(hip_device);
   hipStream_t st = (hipStream_t)stream;
   const bool in_d = is_device_ptr(scores) && is_device_ptr(idx);
@@ -2080,7 +2148,8 @@ int clm_topk_merge(int hip_device, const float* scores, const int64_t* idx, int6
   // every take() rounds its offset up to 256 B: size the workspace by the same rule (a flat
   // +512 slack under-allocated 4 small takes -- found by the host-sanitizer harness)
   const size_t bytes = (in_d ? 0 : round_up(n_in * 4, 256) + round_up(n_in * 8, 256)) +
-                       (out_d ? 0 : round_up((size_t)nq * k * 4, 256) + round_up((size_t)nq * k * 8, 256));
+                       (out_d ? 0 : round_up((size_t)nq * k * 4, 256) + round_up((size_t)nq * k * 8, 256)) +
+                       (any ? round_up(topk_any_ws_bytes(any_rows, k), 256) : 0);
   Scratch& scr = scratch_of_current_device();
   std::unique_lock<std::mutex> lock(scr.mu, std::defer_lock);
   if (bytes > 0) {   // host lists: staged through the device scratch (the call drains its stream)
@@ -2103,12 +2172,21 @@ int clm_topk_merge(int hip_device, const float* scores, const int64_t* idx, int6
     s_in = a; i_in = b;
   }
   if (!out_d) { s_out = (float*)take((size_t)nq * k * 4); i_out = (int64_t*)take((size_t)nq * k * 8); }
-  if (e == hipSuccess) e = topk_merge(s_in, i_in, nq, parts, k_in, k, s_out, i_out, st);
+  if (!any) {
+    if (e == hipSuccess) e = topk_merge(s_in, i_in, nq, parts, k_in, k, s_out, i_out, st);
+  } else {
+    void* aws = take(topk_any_ws_bytes(any_rows, k));
+    const int64_t n_row = (int64_t)parts * k_in;
+    for (int64_t q0 = 0; e == hipSuccess && q0 < nq; q0 += any_rows)
+      e = topk_any(s_in + q0 * n_row, n_row, i_in + q0 * n_row, n_row, std::min(any_rows, nq - q0), n_row, k, 0,
+                   s_out + q0 * k, i_out + q0 * k, k, aws, st);
+  }
   if (e == hipSuccess && !out_d) {
     e = hipMemcpyAsync(out_scores, s_out, (size_t)nq * k * 4, hipMemcpyDeviceToHost, st);
     if (e == hipSuccess) e = hipMemcpyAsync(out_idx, i_out, (size_t)nq * k * 8, hipMemcpyDeviceToHost, st);
   }
-  if (e == hipSuccess && (!in_d || !out_d)) e = hipStreamSynchronize(st);
+  if (e == hipSuccess && bytes > 0) e = hipStreamSynchronize(st);   // the scratch is free again
+  if (bytes > 0) scratch_trim(scr);
   if (e != hipSuccess) return fail(CLM_E_HIP, std::string("topk_merge: ") + hipGetErrorString(e));
   return CLM_OK;
 }
@@ -2130,6 +2208,7 @@ int clm_l2_normalize(int hip_device, float* rows, int64_t n, int dim, void* stre
   if (e == hipSuccess) e = l2_normalize_rows(t, n, dim, st);
   if (e == hipSuccess) e = hipMemcpyAsync(rows, t, (size_t)n * dim * 4, hipMemcpyDeviceToHost, st);
   if (e == hipSuccess) e = hipStreamSynchronize(st);
+  scratch_trim(scr);
   if (e != hipSuccess) return fail(CLM_E_HIP, std::string("l2_normalize: ") + hipGetErrorString(e));
   return CLM_OK;
 }
@@ -2158,6 +2237,7 @@ int clm_fuse_queries(int hip_device, const float* a, float w_a, const float* b, 
   if (e == hipSuccess) e = fuse_rows(t, w_a, tb, w_b, n, dim, t, st);
   if (e == hipSuccess) e = hipMemcpyAsync(out, t, bytes, hipMemcpyDeviceToHost, st);
   if (e == hipSuccess) e = hipStreamSynchronize(st);
+  scratch_trim(scr);
   if (e != hipSuccess) return fail(CLM_E_HIP, std::string("fuse_queries: ") + hipGetErrorString(e));
   return CLM_OK;
 }
@@ -2296,6 +2376,7 @@ extern "C" int clm_resize_crop(int hip_device, const uint8_t* src, const int64_t
   if (e == hipSuccess && !od) e = hipMemcpyAsync(out, d_out, out_bytes, hipMemcpyDeviceToHost, st);
   // the tables live in host vectors and the workspace is freed below: wait for the stream
   if (e == hipSuccess) e = hipStreamSynchronize(st);
+  scratch_trim(scr);
   if (e != hipSuccess) return fail(CLM_E_HIP, std::string("resize_crop: ") + hipGetErrorString(e));
   return CLM_OK;
 }

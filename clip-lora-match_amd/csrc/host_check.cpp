@@ -57,7 +57,7 @@ static void argument_checks() {
   CHECK(clm_encode_text(nullptr, nullptr, 1, 77, nullptr, CLM_F32, 1, nullptr) != CLM_OK);
   clm_index* idx = nullptr;
   CHECK(clm_index_create(0, 16, 100, &idx) != CLM_OK);    // dim % 64 != 0
-  CHECK(clm_index_create(0, 16, 2048, &idx) != CLM_OK);   // dim > 1024
+  CHECK(clm_index_create(0, 16, 131072, &idx) != CLM_OK);   // dim > 65536
   CHECK(clm_index_destroy(nullptr) == CLM_OK);
   CHECK(clm_index_size(nullptr) < 0);
   CHECK(clm_index_search(nullptr, nullptr, CLM_F32, 1, 1, nullptr, nullptr, nullptr) != CLM_OK);
@@ -193,6 +193,34 @@ static void device_checks() {
   CHECK(clm_topk_merge(0, ms.data(), mi.data(), 1, parts, kin, km, os.data(), oi.data(), nullptr) == CLM_OK);
   const int64_t want[km] = {3, 4, 2, 9, 1};
   for (int t = 0; t < km; ++t) CHECK(oi[t] == want[t]);
+
+  // a merge past one LDS sort (topk_any): 5 lists of 3000 with ties and empty slots, k = 4500,
+  // against a host sort by (score desc, index asc)
+  {
+    const int P = 5, KI = 3000, K = 4500, NQ = 2;
+    std::vector<float> bs((size_t)NQ * P * KI);
+    std::vector<int64_t> bi(bs.size());
+    for (size_t j = 0; j < bs.size(); ++j) {
+      bs[j] = (float)((int)(frand() * 64.f)) / 64.f;   // many exact ties
+      bi[j] = (j % 997 == 5) ? -1 : (int64_t)((j * 7919) % 1000003);
+    }
+    std::vector<float> bos((size_t)NQ * K);
+    std::vector<int64_t> boi((size_t)NQ * K);
+    CHECK(clm_topk_merge(0, bs.data(), bi.data(), NQ, P, KI, K, bos.data(), boi.data(), nullptr) == CLM_OK);
+    for (int q = 0; q < NQ; ++q) {
+      std::vector<std::pair<float, int64_t>> v;
+      for (int j = 0; j < P * KI; ++j) {
+        const size_t o = (size_t)q * P * KI + j;
+        if (bi[o] >= 0) v.push_back({bs[o], bi[o]});
+      }
+      std::sort(v.begin(), v.end(), [](const std::pair<float, int64_t>& x, const std::pair<float, int64_t>& y) {
+        return x.first != y.first ? x.first > y.first : x.second < y.second;
+      });
+      int bad = 0;
+      for (int t = 0; t < K; ++t) bad += (boi[(size_t)q * K + t] != v[t].second || bos[(size_t)q * K + t] != v[t].first);
+      CHECK(bad == 0);
+    }
+  }
 
   // l2 normalise and query fusion in place on host rows
   std::vector<float> a((size_t)3 * dim), b((size_t)3 * dim);

@@ -13,6 +13,8 @@
 // CAP keeps its smallest indices), and a bitonic sort of 64-bit
 // (key, ~index) composites in LDS emits the sorted k.
 // topk_merge: sort of parts*k_in candidates per row (chunk / shard merge).
+#include <algorithm>
+
 #include "kernels.hpp"
 
 namespace clm {
@@ -461,7 +463,239 @@ __global__ __launch_bounds__(NT) void topk_merge_kernel(const float* in_s, const
     oi[row * k + j] = (int64_t)(0xFFFFFFFFu - (uint32_t)(v & 0xFFFFFFFFu));
   }
 }
+// ---- top-k for any k (topk_any: k > 1024, or more merge candidates than one LDS sort holds) ----------
+// Every entry's 64-bit composite is (key << 32) | (0xFFFFFFFF - global index): descending composite
+// order is (score desc, index asc).
+// 1. kth_exact_kernel: per row, the exact kk-th largest composite (kk = min(k, C)) as two 32-bit
+//    radix selects (11 / 11 / 10-bit passes each): the key T of the kk-th entry, then among the
+//    entries with key T the low word Lo of the one that is kk-th overall (ties on the score are
+//    broken by the global index whatever order the columns hold them in -- merge inputs are lists).
+// 2. collect_kernel: every composite >= (T, Lo) of the row -- exactly kk -- into a segment of Kp (a
+//    power of two) u64, 0-padded (order irrelevant).
+// 3. sort_runs_kernel: LDS bitonic sort (descending) of runs of min(Kp, RUN); merge_runs_kernel:
+//    merge passes doubling the run length until it is Kp (merge path by binary search, stable:
+//    equal composites -- only the 0 pads -- keep A before B).
+// 4. emit_kernel: the first k composites as (score, global index), (-inf, -1) for pads.
+constexpr int RUN = 8192;
+
+__device__ __forceinline__ bool any_valid(const int64_t* ix, int64_t j) { return !ix || ix[j] >= 0; }
+__device__ __forceinline__ uint32_t any_lo(const int64_t* ix, int64_t base, int64_t j) {
+  return 0xFFFFFFFFu - (uint32_t)(ix ? ix[j] : base + j);
+}
+
+// radix select over `get(i, v)` (true: entry i takes part with 32-bit value v) of the kk-th largest
+// value, three passes 11 / 11 / 10 bits; returns the value and the number of entries equal to it
+// that belong to the top kk (s_kk). All threads of the block call it.
+template <typename Get>
+__device__ void radix_kth(int64_t C, int kk, uint32_t* hist, uint32_t& s_prefix, int& s_pbits, int& s_kk, Get get) {
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  if (tid == 0) { s_prefix = 0; s_pbits = 0; s_kk = kk; }
+  __syncthreads();
+  for (int pass = 0; pass < 3; ++pass) {
+    const int pbits = s_pbits;
+    const uint32_t prefix = s_prefix;
+    const int width = pass < 2 ? 11 : 10;
+    const int shift = 32 - pbits - width;
+    const int nb = 1 << width;
+    for (int i = tid; i < nb; i += NT) hist[i] = 0;
+    __syncthreads();
+    for (int64_t i = tid; i < C; i += NT) {
+      uint32_t v;
+      if (get(i, v) && (pbits == 0 || (v >> (32 - pbits)) == prefix)) atomicAdd(&hist[(v >> shift) & (nb - 1)], 1u);
+    }
+    __syncthreads();
+    if (wid == 0) {   // the bin (from the top) holding the kk-th value, as topk_rows_kernel
+      const int per = nb / 64;
+      const int hi_bin = nb - 1 - lane * per;
+      int gs = 0;
+      for (int q = 0; q < per; ++q) gs += hist[hi_bin - q];
+      int cum = gs;
+      for (int o = 1; o < 64; o <<= 1) {
+        const int v = __shfl_up(cum, o, 64);
+        if (lane >= o) cum += v;
+      }
+      const int k2 = s_kk;
+      const unsigned long long m = __ballot(cum >= k2);
+      const int first = m ? __ffsll((long long)m) - 1 : 63;
+      if (lane == first) {
+        int above = cum - gs;
+        int bin = hi_bin;
+        for (int q = 0; q < per; ++q) {
+          const int b = hi_bin - q;
+          if (above + (int)hist[b] >= k2 || q == per - 1) { bin = b; break; }
+          above += hist[b];
+        }
+        s_kk = k2 - above;
+        s_prefix = (prefix << width) | (uint32_t)bin;
+        s_pbits = pbits + width;
+      }
+    }
+    __syncthreads();
+  }
+}
+
+__global__ __launch_bounds__(NT) void kth_exact_kernel(const float* S, int64_t lds, const int64_t* I, int64_t ldi,
+                                                       int64_t C, int k, int64_t base, uint32_t* thr) {
+  __shared__ uint32_t hist[2048];
+  __shared__ uint32_t s_prefix;
+  __shared__ int s_pbits, s_kk;
+  const int64_t row = blockIdx.x;
+  const float* s = S + row * lds;
+  const int64_t* ix = I ? I + row * ldi : nullptr;
+  int64_t nvalid = C;
+  if (ix) {   // entries that can be taken (empty merge slots cannot)
+    __shared__ int s_nv;
+    if (threadIdx.x == 0) s_nv = 0;
+    __syncthreads();
+    int c = 0;
+    for (int64_t i = threadIdx.x; i < C; i += NT) c += ix[i] >= 0;
+    atomicAdd(&s_nv, c);
+    __syncthreads();
+    nvalid = s_nv;
+  }
+  const int kk = (int)min((int64_t)k, nvalid);
+  if (kk <= 0) {   // nothing to take: a threshold above every composite
+    if (threadIdx.x == 0) { thr[2 * row] = 0xFFFFFFFFu; thr[2 * row + 1] = 0xFFFFFFFFu; }
+    return;
+  }
+  radix_kth(C, kk, hist, s_prefix, s_pbits, s_kk, [&](int64_t i, uint32_t& v) {
+    if (!any_valid(ix, i)) return false;
+    v = fkey(s[i]);
+    return true;
+  });
+  const uint32_t T = s_prefix;
+  const int need = s_kk;
+  __syncthreads();
+  radix_kth(C, need, hist, s_prefix, s_pbits, s_kk, [&](int64_t i, uint32_t& v) {
+    if (!any_valid(ix, i) || fkey(s[i]) != T) return false;
+    v = any_lo(ix, base, i);
+    return true;
+  });
+  if (threadIdx.x == 0) { thr[2 * row] = T; thr[2 * row + 1] = s_prefix; }
+}
+
+__global__ __launch_bounds__(NT) void collect_kernel(const float* S, int64_t lds, const int64_t* I, int64_t ldi,
+                                                     int64_t C, int64_t base, const uint32_t* thr, uint64_t* seg,
+                                                     int64_t Kp) {
+  __shared__ int s_n;
+  const int64_t row = blockIdx.x;
+  const float* s = S + row * lds;
+  const int64_t* ix = I ? I + row * ldi : nullptr;
+  uint64_t* out = seg + row * Kp;
+  for (int64_t j = threadIdx.x; j < Kp; j += NT) out[j] = 0;
+  if (threadIdx.x == 0) s_n = 0;
+  __syncthreads();
+  const uint64_t lim = ((uint64_t)thr[2 * row] << 32) | thr[2 * row + 1];
+  for (int64_t i = threadIdx.x; i < C; i += NT) {
+    if (!any_valid(ix, i)) continue;
+    const uint64_t comp = ((uint64_t)fkey(s[i]) << 32) | any_lo(ix, base, i);
+    if (comp >= lim) {
+      const int at = atomicAdd(&s_n, 1);
+      if (at < Kp) out[at] = comp;
+    }
+  }
+}
+
+__global__ __launch_bounds__(NT) void sort_runs_kernel(uint64_t* seg, int64_t Kp, int run) {
+  __shared__ uint64_t a[RUN];
+  uint64_t* p = seg + (int64_t)blockIdx.y * Kp + (int64_t)blockIdx.x * run;
+  for (int j = threadIdx.x; j < run; j += NT) a[j] = p[j];
+  __syncthreads();
+  bitonic_desc(a, run);
+  for (int j = threadIdx.x; j < run; j += NT) p[j] = a[j];
+}
+
+__global__ __launch_bounds__(256) void merge_runs_kernel(const uint64_t* src, uint64_t* dst, int64_t Kp, int64_t L,
+                                                         int64_t total) {
+  for (int64_t p = (int64_t)blockIdx.x * 256 + threadIdx.x; p < total; p += (int64_t)gridDim.x * 256) {
+    const int64_t row = p / Kp, q = p - row * Kp;
+    const int64_t r = q / L, pos = q - r * L;
+    const uint64_t x = src[p];
+    const uint64_t* other = src + row * Kp + (r ^ 1) * L;
+    const bool b_side = r & 1;
+    int64_t lo = 0, hi = L;   // other-run elements that precede x: > x (x in A) or >= x (x in B)
+    while (lo < hi) {
+      const int64_t mid = (lo + hi) >> 1;
+      const uint64_t o = other[mid];
+      if (b_side ? o >= x : o > x) lo = mid + 1;
+      else hi = mid;
+    }
+    dst[row * Kp + (r & ~(int64_t)1) * L + pos + lo] = x;
+  }
+}
+
+__global__ __launch_bounds__(256) void emit_kernel(const uint64_t* seg, int64_t Kp, int64_t nq, int k, float* os,
+                                                   int64_t* oi, int64_t ldo) {
+  const int64_t total = nq * k;
+  for (int64_t p = (int64_t)blockIdx.x * 256 + threadIdx.x; p < total; p += (int64_t)gridDim.x * 256) {
+    const int64_t row = p / k, j = p - row * k;
+    const uint64_t v = j < Kp ? seg[row * Kp + j] : 0;
+    if (v == 0) {
+      os[row * ldo + j] = -INFINITY;
+      oi[row * ldo + j] = -1;
+    } else {
+      os[row * ldo + j] = kfloat((uint32_t)(v >> 32));
+      oi[row * ldo + j] = (int64_t)(0xFFFFFFFFu - (uint32_t)(v & 0xFFFFFFFFu));
+    }
+  }
+}
+
+int64_t any_kp(int k) {
+  int64_t kp = 2;
+  while (kp < k) kp <<= 1;
+  return kp;
+}
 }  // namespace
+
+size_t topk_any_ws_bytes(int64_t nq, int k) {
+  const int64_t kp = any_kp(k);
+  return (size_t)nq * 8 + 256 + 2 * (size_t)nq * kp * 8;
+}
+
+hipError_t topk_any(const float* scores, int64_t lds, const int64_t* idx, int64_t ldi, int64_t nq, int64_t C, int k,
+                    int64_t base, float* out_s, int64_t* out_i, int64_t ldo, void* ws, hipStream_t s) {
+  if (nq <= 0) return hipSuccess;
+  if (k < 1 || C < 0 || C > 0xFFFFFFFFll || nq > 65535 || !ws) return hipErrorInvalidValue;
+  const int64_t kp = any_kp(k);
+  uint32_t* thr = (uint32_t*)ws;   // per row {T, Lo}
+  uint64_t* seg = (uint64_t*)(((uintptr_t)(thr + 2 * nq) + 255) & ~(uintptr_t)255);
+  uint64_t* seg2 = seg + nq * kp;
+  kth_exact_kernel<<<(unsigned)nq, NT, 0, s>>>(scores, lds, idx, ldi, C, k, base, thr);
+  collect_kernel<<<(unsigned)nq, NT, 0, s>>>(scores, lds, idx, ldi, C, base, thr, seg, kp);
+  const int run = (int)std::min<int64_t>(kp, RUN);
+  sort_runs_kernel<<<dim3((unsigned)(kp / run), (unsigned)nq), NT, 0, s>>>(seg, kp, run);
+  uint64_t *a = seg, *b = seg2;
+  for (int64_t L = run; L < kp; L <<= 1) {
+    const int64_t total = nq * kp;
+    merge_runs_kernel<<<(unsigned)std::min<int64_t>((total + 255) / 256, 65536), 256, 0, s>>>(a, b, kp, L, total);
+    std::swap(a, b);
+  }
+  emit_kernel<<<(unsigned)std::min<int64_t>((nq * k + 255) / 256, 65536), 256, 0, s>>>(a, kp, nq, k, out_s, out_i, ldo);
+  return hipGetLastError();
+}
+
+namespace {
+// cnt[row] = #{ j < C : S[row, j] >= th[row] } (one 256-thread workgroup per row)
+__global__ __launch_bounds__(256) void count_ge_kernel(const float* S, int64_t lds, int64_t C, const float* th,
+                                                       int* cnt) {
+  __shared__ int part[4];
+  const int64_t row = blockIdx.x;
+  const float t = th[row];
+  const float* s = S + row * lds;
+  int c = 0;
+  for (int64_t j = threadIdx.x; j < C; j += 256) c += s[j] >= t;
+  for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
+  if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = c;
+  __syncthreads();
+  if (threadIdx.x == 0) cnt[row] = part[0] + part[1] + part[2] + part[3];
+}
+}  // namespace
+
+hipError_t count_ge(const float* scores, int64_t lds, int64_t nq, int64_t C, const float* th, int* cnt, hipStream_t s) {
+  if (nq <= 0) return hipSuccess;
+  count_ge_kernel<<<(unsigned)nq, 256, 0, s>>>(scores, lds, C, th, cnt);
+  return hipGetLastError();
+}
 
 hipError_t topk_rows(const float* scores, int64_t lds, int64_t nq, int64_t C, int k, int64_t base, float* out_s,
                      int64_t* out_i, int64_t ldo, hipStream_t s) {

@@ -189,6 +189,16 @@ hipError_t rows_to_f16(const void* src, int src_dtype, int64_t n, int dim, u16* 
 // idx asc); idx = base + column.
 hipError_t topk_rows(const float* scores, int64_t lds, int64_t nq, int64_t C, int k,
                      int64_t base, float* out_s, int64_t* out_i, int64_t ldo, hipStream_t s);
+// top-k of any k (k > 1024, or candidate lists longer than one LDS sort): exact k-th key by radix
+// select, the k composites collected, sorted (LDS runs + merge passes), emitted. idx == null: the
+// global index of column j is base + j; else idx[row * ldi + j] (< 0: an empty slot, never taken
+// before a score). Rows with fewer than k entries end in (-inf, -1). nq <= 65535; ws of
+// topk_any_ws_bytes(nq, k) device bytes.
+size_t topk_any_ws_bytes(int64_t nq, int k);
+hipError_t topk_any(const float* scores, int64_t lds, const int64_t* idx, int64_t ldi, int64_t nq, int64_t C, int k,
+                    int64_t base, float* out_s, int64_t* out_i, int64_t ldo, void* ws, hipStream_t s);
+// cnt[q] = number of scores in row q [C] (row stride lds) that are >= th[q]
+hipError_t count_ge(const float* scores, int64_t lds, int64_t nq, int64_t C, const float* th, int* cnt, hipStream_t s);
 // merge `parts` candidate lists per row: in [nq, parts*k_in] -> out [nq, k]
 hipError_t topk_merge(const float* in_s, const int64_t* in_i, int64_t nq, int parts, int k_in,
                       int k, float* out_s, int64_t* out_i, hipStream_t s);

@@ -118,7 +118,7 @@ def _save_index(rows: torch.Tensor, descriptions: Sequence, image_paths: Sequenc
 def rebuild_index(model, processor, descriptions: Sequence, image_paths: Sequence[str],
                   index_path: Union[str, Path], batch_size: int = 256, from_images: bool = False,
                   group=None, images=None, exchange: str = "fp32",
-                  host_rows: Optional[bool] = None) -> torch.Tensor:
+                  host_rows: bool = True) -> torch.Tensor:
     """rebuild_index.py:28-115: embed every item (its description by default, as the reference
     does; its image with from_images=True -- the files at image_paths, or `images`: any image
     source encode_items takes, e.g. pixels already on the device), save the .pt index, return the
@@ -126,9 +126,10 @@ def rebuild_index(model, processor, descriptions: Sequence, image_paths: Sequenc
     renamed into place); its outcome is broadcast, so every rank returns after the file exists or
     raises if rank 0's write failed (no rank is left waiting). No items: nothing is written (:54-56).
 
-    Only the writing process copies the rows to the host: it returns the CPU rows, the other ranks
-    return the gathered rows on their device (2 GB of D2H per rank saved at 1 M rows); host_rows=True
-    returns CPU rows on every rank, False device rows everywhere. exchange: see encode_items."""
+    Every rank returns the CPU rows by default (host_rows=True, the reference's return type);
+    host_rows=False returns the gathered rows on each rank's device instead, so only the writing
+    process copies them to the host (2 GB of D2H per rank saved at 1 M rows). exchange: see
+    encode_items."""
     if len(descriptions) != len(image_paths):
         raise ValueError(f"{len(descriptions)} descriptions vs {len(image_paths)} image paths")
     if images is not None and len(images) != len(image_paths):
@@ -160,9 +161,9 @@ def rebuild_index(model, processor, descriptions: Sequence, image_paths: Sequenc
                                    group=group)
         if status[0] is not None:
             raise RuntimeError(status[0])
-    if host_rows is None:
-        return rows
-    return (rows if writer else dev_rows.cpu()) if host_rows else dev_rows
+    if host_rows:
+        return rows if writer else dev_rows.cpu()
+    return dev_rows
 
 
 __all__ = ["encode_items", "rebuild_index", "fold_sha256"]

@@ -181,11 +181,14 @@ class CosineIndex:
     def stats(self) -> dict:
         """queries served by the sampled single-pass bounded search (`filtered`), the bounded
         search with a chunked fp16 scan as its first step (`scan_bounded`), the full exact
-        scan (`full_exact`), their sum `exact`, and overflow re-runs (include/clm.h)"""
-        v = (ctypes.c_int64 * 4)()
-        C.check(C.lib().clm_index_stats2(self._h, v, 4))
+        scan (`full_exact`), their sum `exact`, overflow re-runs, and the queries whose filter
+        pass ran on the G2 256 x 192 tiles (`filter_g2`) or, in blocks whose sampled candidate
+        windows mostly exceed the list capacity, on gemm_kernel 256 x 256 (`filter_dense`)
+        (include/clm.h)"""
+        v = (ctypes.c_int64 * 6)()
+        C.check(C.lib().clm_index_stats2(self._h, v, 6))
         return {"filtered": v[0], "scan_bounded": v[1], "full_exact": v[2], "exact": v[1] + v[2],
-                "overflow": v[3]}
+                "overflow": v[3], "filter_g2": v[4], "filter_dense": v[5]}
 
     def close(self) -> None:
         if getattr(self, "_h", None):
@@ -303,8 +306,6 @@ class TextSearchIndex:
             q = torch.as_tensor(queries)
             nq = 1 if q.dim() == 1 else q.shape[0]
             return torch.empty((nq, 0)), torch.empty((nq, 0), dtype=torch.int64)
-        if k > 1024:
-            raise ValueError("top_k > 1024 is not supported by the GPU top-k kernel")
         return self._gpu.search(queries, k)
 
     def search_with_embedding(self, query_emb: torch.Tensor, top_k: int = 5) -> List[SearchResult]:

@@ -192,7 +192,9 @@ int clm_index_search(clm_index* idx, const void* q, int q_dtype, int64_t nq, int
  * bounded queries whose candidate list overflowed (redone by a whole-list pass, or by the exact
  * scan when the list is longer than 8192 / k chunks of 4096) */
 int clm_index_stats(const clm_index* idx, int64_t* filtered, int64_t* exact, int64_t* overflow);
-/* out[0..n): sampled bounded, fp16-scan bounded, full exact scan, overflow re-runs */
+/* out[0..n), n <= 6: sampled bounded, fp16-scan bounded, full exact scan, overflow re-runs, then the
+ * sampled queries whose filter pass ran on the G2 256 x 192 tiles / on gemm_kernel 256 x 256 (chosen
+ * per query block from the block's sampled candidate counts: near-duplicate blocks take the latter) */
 int clm_index_stats2(const clm_index* idx, int64_t* out, int n);
 
 /* full cosine matrix, exact: out [nq, n] f32 = fp32(cos64(q_i, c_j)), any dim */

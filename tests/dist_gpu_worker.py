@@ -19,7 +19,7 @@ from clip_lora_match_amd import synthetic as syn  # noqa: E402
 from clip_lora_match_amd import weights as W  # noqa: E402
 from clip_lora_match_amd.distributed import ShardedIndex, merge_topk_gpu  # noqa: E402
 from clip_lora_match_amd.engine import ClipLoraModel  # noqa: E402
-from clip_lora_match_amd.index_build import _renormalize, encode_items, rebuild_index  # noqa: E402
+from clip_lora_match_amd.index_build import _f16_exchange, _f16_restore, _renormalize, encode_items, rebuild_index  # noqa: E402
 from clip_lora_match_amd.processor import ClipProcessor  # noqa: E402
 from clip_lora_match_amd.search import CosineIndex  # noqa: E402
 
@@ -68,6 +68,10 @@ def main(out_path, tmpdir):
     names = [f"synthetic/{i:06d}.png" for i in range(n_big)]
     e_big = rebuild_index(big, proc, [""] * n_big, names, os.path.join(tmpdir, "big.pt"), batch_size=256,
                           from_images=True, images=src)
+    # the fp16 all_gather exchange (half the link bytes): the fp32 rows rounded to fp16 and
+    # re-normalised in fp32 after the gather, on every rank
+    e_big16 = rebuild_index(big, proc, [""] * n_big, names, os.path.join(tmpdir, "big16.pt"), batch_size=256,
+                            from_images=True, images=src, exchange="fp16", host_rows=False)
     big_file = torch.load(os.path.join(tmpdir, "big.pt"), map_location="cpu", weights_only=True)
     # 4. a failed write on rank 0 raises on every rank (nobody is left in a collective)
     blocker = os.path.join(tmpdir, "not_a_dir")
@@ -89,6 +93,8 @@ def main(out_path, tmpdir):
         ref_big = torch.cat([_renormalize(big.encode_pixels(src.batch(a, min(a + 200, n_big))))
                              for a in range(0, n_big, 200)]).cpu()
         res["big_build_equal"] = bool(torch.equal(e_big, ref_big))
+        res["big_f16_exchange_equal"] = bool(torch.equal(e_big16.cpu(), _f16_restore(_f16_exchange(ref_big.cuda())).cpu()))
+        res["big_f16_exchange_device"] = str(e_big16.device)
         res["big_file_equal"] = bool(torch.equal(big_file["embeddings"], ref_big))
         res["big_file_rows"] = int(big_file["embeddings"].shape[0])
         res["big_paths_ok"] = big_file["image_paths"][12345] == names[12345]

@@ -1,9 +1,11 @@
 """Worker of tests/test_gpu_distributed.py::test_index_build_1m_*: BASELINE configs[2] at its
 stated size -- rebuild_index(from_images=True) over 1,000,000 device-generated 224^2 images
-(synthetic.DeviceImages, pixels a function of the global row), ViT-B/32 + LoRA, fp16, batch 512,
-with the fp16 all_gather exchange -- at whatever world size torch.distributed.run started (gloo:
-the 1-GPU box rehearses world 2 on one device). Rank 0 reloads the .pt and writes a JSON verdict:
-the fold checksum of the returned rows and of the file, rows, and spot-checked image paths."""
+(synthetic.DeviceImages, pixels a function of the global row), ViT-B/32 + LoRA at the given
+compute dtype (the bench headline's "mixed"), batch 512, with the given all_gather exchange (fp32,
+bench.py's configs[2] headline) -- at whatever world size torch.distributed.run started (gloo: the
+1-GPU box rehearses world 2 on one device). Rank 0 reloads the .pt and writes a JSON verdict: the
+fold checksum of the returned rows and of the file, rows, spot-checked image paths, and 64 of the
+rows (spread over the index) copied out for the oracle spot check."""
 import json
 import os
 import sys
@@ -23,14 +25,17 @@ from clip_lora_match_amd.index_build import fold_sha256, rebuild_index  # noqa: 
 from clip_lora_match_amd.processor import ClipProcessor  # noqa: E402
 
 
-def main(out_path, tmpdir, n, exchange):
+SPOT = [0, 1, 511, 512, 99_999, 123_457, 500_000, 999_999] + [7_919 * j + 13 for j in range(1, 57)]
+
+
+def main(out_path, tmpdir, n, exchange, dtype):
     torch.cuda.set_device(0)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if world > 1:
         dist.init_process_group("gloo")
     rank = dist.get_rank() if world > 1 else 0
     cfg = clm.get_preset("ViT-B/32")
-    model = ClipLoraModel(cfg, compute_dtype="float16", max_batch=512)
+    model = ClipLoraModel(cfg, compute_dtype=dtype, max_batch=512)
     model.load_tensors(W.synthetic_state_dict(cfg, 0))
     model.load_tensors(W.synthetic_lora(cfg, 1))
     model.finalize()
@@ -39,7 +44,7 @@ def main(out_path, tmpdir, n, exchange):
     path = os.path.join(tmpdir, f"index_w{world}.pt")
     t0 = time.perf_counter()
     rows = rebuild_index(model, ClipProcessor(cfg), [""] * n, names, path, batch_size=512, from_images=True,
-                         images=src, exchange=exchange)
+                         images=src, exchange=exchange, host_rows=False)
     dt = time.perf_counter() - t0
     res = {"world": world, "rank": rank, "seconds": round(dt, 2), "rows_device": str(rows.device),
            "rows_shape": list(rows.shape), "rows_sha": fold_sha256(rows)}
@@ -48,6 +53,9 @@ def main(out_path, tmpdir, n, exchange):
         dist.all_gather_object(shas, res["rows_sha"])
         res["rank_shas"] = shas
     if rank == 0:
+        spot = [i for i in SPOT if i < n]
+        res["spot_rows"] = spot
+        res["spot_emb"] = rows[spot].cpu().tolist()
         obj = torch.load(path, map_location="cpu", weights_only=True)
         emb = obj["embeddings"]
         res.update({"file_rows": int(emb.shape[0]), "file_dtype": str(emb.dtype), "file_sha": fold_sha256(emb),
@@ -65,4 +73,4 @@ def main(out_path, tmpdir, n, exchange):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1], sys.argv[2], int(sys.argv[3]), sys.argv[4])
+    main(sys.argv[1], sys.argv[2], int(sys.argv[3]), sys.argv[4], sys.argv[5])

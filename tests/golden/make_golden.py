@@ -200,8 +200,42 @@ def search_fp32_golden():
     print("search_fp32.npz")
 
 
+def search_large_golden():
+    """k > 1024 (up to k = N and past it: torch.topk takes min(k, N)) and dim > 1024 through the
+    reference's own similarity.top_k_similar: the first 4 queries of the fp32 Gaussian and clustered
+    sets at k = 1025, 2000, 4096 = N (indices fit int16), and 8 queries on 2048 Gaussian fp32 rows of
+    dim 1536 at k = 5, 50, 1500."""
+    sim = _load_ref_similarity()
+    gauss_rows, gauss_q, clus, clus_q = syn.fp32_search_inputs()
+    out = {}
+    for name, rows, qs in (("gauss", gauss_rows, gauss_q), ("clus", clus, clus_q)):
+        E = torch.from_numpy(rows)
+        for k in (1025, 2000, 4096):
+            vals = np.zeros((4, k), np.float32)
+            idx = np.zeros((4, k), np.int16)
+            for i in range(4):
+                v, ix = sim.top_k_similar(torch.from_numpy(qs[i]), E, k)
+                vals[i], idx[i] = v.numpy(), ix.numpy().astype(np.int16)
+            out[f"{name}_vals_k{k}"] = vals
+            out[f"{name}_idx_k{k}"] = idx
+    wide_rows = syn.gaussian_rows(2048, 1536, seed=31, fp16=False)
+    wide_q = syn.gaussian_rows(8, 1536, seed=32, fp16=False)
+    E = torch.from_numpy(wide_rows)
+    for k in (5, 50, 1500):
+        vals = np.zeros((8, k), np.float32)
+        idx = np.zeros((8, k), np.int16)
+        for i in range(8):
+            v, ix = sim.top_k_similar(torch.from_numpy(wide_q[i]), E, k)
+            vals[i], idx[i] = v.numpy(), ix.numpy().astype(np.int16)
+        out[f"wide_vals_k{k}"] = vals
+        out[f"wide_idx_k{k}"] = idx
+    out["wide_seeds"] = np.array([31, 32])
+    np.savez_compressed(os.path.join(HERE, "search_large_k.npz"), **out)
+    print("search_large_k.npz")
+
+
 if __name__ == "__main__":
-    which = sys.argv[1:] or ["tiny", "b32", "b32_64", "l14", "search", "search_fp32", "images"]
+    which = sys.argv[1:] or ["tiny", "b32", "b32_64", "l14", "search", "search_fp32", "search_large", "images"]
     if "tiny" in which:
         encoder_golden("enc_tiny_lora.npz", "tiny", 4, 4, 16, True)
     if "b32" in which:
@@ -214,5 +248,7 @@ if __name__ == "__main__":
         search_golden()
     if "search_fp32" in which:
         search_fp32_golden()
+    if "search_large" in which:
+        search_large_golden()
     if "images" in which:
         image_golden()

@@ -35,19 +35,26 @@ def test_sharded_build_and_search_world2(tmp_path):
     assert r["file_rows_min_max"] == [37, 37]     # both ranks read the complete file
     for key in ("build_img_equal", "build_txt_equal", "file_equal", "search_idx_equal", "search_scores_equal",
                 "merge_roundtrip", "big_build_equal", "big_file_equal", "big_paths_ok", "synth_rows_stable",
+                "big_f16_exchange_equal",
                 "write_failure_raised_everywhere"):
         assert r[key], (key, r)
     assert r["planted_top1"] == [5, 150_000, 150_001, 299_999]
     assert r["big_file_rows"] == 65_536
+    assert r["big_f16_exchange_device"].startswith("cuda")   # host_rows=False: device rows on every rank
 
 
 N_1M = 1_000_000
 
 
+# bench.py's configs[2] leg: the headline compute dtype and the fp32 all_gather exchange; its
+# index_fold_sha256 line equals the world-1 checksum of this build (rows do not depend on the batch)
+INDEX_DTYPE, INDEX_EXCHANGE = "mixed", "fp32"
+
+
 @pytest.fixture(scope="module")
 def index_1m(tmp_path_factory):
-    """configs[2] at its stated size (rebuild_index over 1 M device-generated images, fp16 all_gather
-    exchange), run once per world size {1, 2} by tests/dist_index_worker.py; results by world."""
+    """configs[2] at its stated size (rebuild_index over 1 M device-generated images at the bench's
+    dtype and exchange), run once per world size {1, 2} by tests/dist_index_worker.py; results by world."""
     d = tmp_path_factory.mktemp("index_1m")
     return {"dir": d, "res": {}}
 
@@ -56,7 +63,7 @@ def _run_index_1m(index_1m, world):
     out = index_1m["dir"] / f"w{world}.json"
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
            "--master-addr=127.0.0.1", f"--master-port={_port()}", os.path.join(REPO, "tests", "dist_index_worker.py"),
-           str(out), str(index_1m["dir"]), str(N_1M), "fp16"]
+           str(out), str(index_1m["dir"]), str(N_1M), INDEX_EXCHANGE, INDEX_DTYPE]
     p = subprocess.run(cmd, env=dict(os.environ, MASTER_ADDR="127.0.0.1"), capture_output=True, text=True,
                        timeout=170)
     assert p.returncode == 0, p.stderr[-3000:]
@@ -70,15 +77,41 @@ def test_index_build_1m_world1(index_1m):
     with every image path in place (scripts/rebuild_index.py:64-96)."""
     r = _run_index_1m(index_1m, 1)
     assert r["file_rows"] == N_1M and r["rows_shape"] == [N_1M, 512]
-    assert r["rows_device"] == "cpu"          # the writing process returns host rows
+    assert r["rows_device"].startswith("cuda")   # host_rows=False: the gathered rows stay on the device
     assert r["file_sha"] == r["rows_sha"] and r["file_dtype"] == "torch.float32"
     assert r["paths_ok"] and r["texts_ok"] and r["unit_rows"] < 1e-6
+    print(f"\nconfigs[2] 1 M build ({INDEX_DTYPE}, {INDEX_EXCHANGE} exchange): fold {r['rows_sha']}")
+
+
+def test_index_build_1m_spot_vs_oracle(index_1m):
+    """64 rows of the 1 M build (spread over the whole index) against the fp32 oracle
+    (oracle.clip_ref.image_features + the reference's second normalise) on the same device-generated
+    pixels: the headline dtype's bars, 1 - cos <= 1e-4 per row and pairwise scores within 1e-3."""
+    if 1 not in index_1m["res"]:
+        pytest.skip("needs the world-1 result (run the module)")
+    import numpy as np
+    import clip_lora_match_amd as clm
+    from clip_lora_match_amd import synthetic as syn
+    from clip_lora_match_amd import weights as W
+    from oracle import clip_ref as R
+    r = index_1m["res"][1]
+    cfg = clm.get_preset("ViT-B/32")
+    src = syn.DeviceImages(N_1M, cfg.image_size, seed=20240)
+    px = np.stack([src.batch(i, i + 1).cpu().numpy()[0] for i in r["spot_rows"]])
+    ref = R.image_features(W.synthetic_state_dict(cfg, 0), cfg, R.preprocess_u8(px, cfg.mean, cfg.std),
+                           W.synthetic_lora(cfg, 1))
+    ref = ref / np.linalg.norm(ref, axis=1, keepdims=True)
+    got = np.asarray(r["spot_emb"], np.float64)
+    cos = np.sum(got * ref, 1) / (np.linalg.norm(got, axis=1) * np.linalg.norm(ref, axis=1))
+    err = np.max(np.abs(got @ got.T - ref @ ref.T))
+    print(f"\n1 M build spot check: max 1 - cos {np.max(1 - cos):.2e}, max score error {err:.2e}")
+    assert np.max(1 - cos) <= 1e-4 and err <= 1e-3
 
 
 def test_index_build_1m_world2(index_1m):
     """The same build sharded over 2 ranks (gloo on one GPU; RCCL on the 8-GPU node): every rank
-    gathers the same 1 M rows (fp16 exchange), rank 0 keeps them on the host, rank 1 on its
-    device, and the index is bit-identical to the world-1 build (fold checksum)."""
+    gathers the same 1 M rows (on its device, host_rows=False), and the index is bit-identical to
+    the world-1 build (fold checksum)."""
     if 1 not in index_1m["res"]:
         pytest.skip("needs the world-1 result (run the module)")
     r = _run_index_1m(index_1m, 2)

@@ -665,3 +665,111 @@ def test_fp16_shard_roundtrip_and_bad_files(tmp_path):
         CosineIndex.load_shard(tmp_path / "missing.clmidx")
     idx.close()
     re_.close()
+
+
+@pytest.mark.parametrize("name", ["gauss", "clus"])
+def test_large_k_vs_reference_golden(name):
+    """k > 1024 (the exact scan + topk_any: exact k-th key, collection, LDS runs + merge passes)
+    against the reference's own top_k_similar at k = 1025, 2000, 4096 = N: indices up to 2e-6
+    near-ties, scores within 1e-6; through CosineIndex, top_k_similar and TextSearchIndex (top_k
+    past N returns all N rows, as min(top_k, N) in search.py:98)."""
+    g = golden("search_large_k.npz")
+    gr, gq, cr, cq = syn.fp32_search_inputs()
+    rows, qs = (gr, gq[:4]) if name == "gauss" else (cr, cq[:4])
+    exact = S.cosine_scores(qs.astype(np.float64), rows.astype(np.float64))
+    idx = CosineIndex(rows.shape[1], capacity=rows.shape[0])
+    idx.append(torch.from_numpy(rows))
+    for k in (1025, 2000, 4096):
+        s, i = idx.search(torch.from_numpy(qs), k)
+        s, i = s.cpu().numpy(), i.cpu().numpy()
+        _agree(i, g[f"{name}_idx_k{k}"].astype(np.int64), exact)
+        assert np.max(np.abs(s - g[f"{name}_vals_k{k}"])) < 1e-6
+        _, oi = S.topk(exact, k)
+        _agree(i, oi, exact)
+        assert len(set(i[0].tolist())) == k
+    v, ix = top_k_similar(torch.from_numpy(qs[1]), torch.from_numpy(rows), 2000)
+    assert v.shape == (2000,) and ix.shape == (2000,)
+    _agree(ix.cpu().numpy()[None], g[f"{name}_idx_k2000"][1:2].astype(np.int64), exact[1:2])
+    tsi = TextSearchIndex(embeddings=torch.from_numpy(rows), image_paths=[f"img{j}" for j in range(rows.shape[0])],
+                          texts=[f"t{j}" for j in range(rows.shape[0])])
+    res = tsi.search_with_embedding(torch.from_numpy(qs[0]), top_k=10_000)
+    assert len(res) == rows.shape[0]
+    got = np.array([r.index for r in res])
+    _agree(got[None], g[f"{name}_idx_k4096"][:1].astype(np.int64), exact[:1])
+    assert res[0].image_path == f"img{got[0]}"
+
+
+@pytest.mark.parametrize("k", [5, 50, 1500])
+def test_wide_dim_vs_reference_golden(k):
+    """dim 1536 > 1024 (the index takes any multiple-of-64 dim up to 65536 after padding; the
+    candidate margin holds to 8192): the reference's top_k_similar goldens, through top_k_similar
+    and a bounded (sampled) CosineIndex search."""
+    g = golden("search_large_k.npz")
+    rows = syn.gaussian_rows(2048, 1536, seed=int(g["wide_seeds"][0]), fp16=False)
+    qs = syn.gaussian_rows(8, 1536, seed=int(g["wide_seeds"][1]), fp16=False)
+    exact = S.cosine_scores(qs.astype(np.float64), rows.astype(np.float64))
+    want = g[f"wide_idx_k{k}"].astype(np.int64)
+    for q in range(2):
+        v, ix = top_k_similar(torch.from_numpy(qs[q]), torch.from_numpy(rows), k)
+        _agree(ix.cpu().numpy()[None], want[q:q + 1], exact[q:q + 1])
+        assert np.max(np.abs(v.cpu().numpy() - g[f"wide_vals_k{k}"][q])) < 1e-6
+    idx = CosineIndex(1536, capacity=2048)
+    idx.append(torch.from_numpy(rows).cuda())
+    import os
+    os.environ["CLM_SEARCH_BOUNDED"] = "1"
+    try:
+        s, i = idx.search(torch.from_numpy(qs).cuda(), k)
+    finally:
+        del os.environ["CLM_SEARCH_BOUNDED"]
+    _agree(i.cpu().numpy(), want, exact)
+    assert np.max(np.abs(s.cpu().numpy() - g[f"wide_vals_k{k}"])) < 1e-6
+
+
+def test_merge_past_one_sort():
+    """merge_topk_gpu / clm_topk_merge with more candidates than one LDS sort (parts * k_in >
+    8192) and k > 1024: the (score desc, index asc) order of the union, empty (-1) slots last."""
+    from clip_lora_match_amd.distributed import merge_topk_gpu
+    g = np.random.default_rng(5)
+    nq, parts, k_in, k = 3, 4, 2500, 3000
+    sc = (g.integers(0, 200, (nq, parts * k_in)) / 200.0).astype(np.float32)   # many ties
+    ix = np.stack([g.permutation(10 * parts * k_in)[:parts * k_in] for _ in range(nq)]).astype(np.int64)
+    ix[:, ::97] = -1
+    s, i = merge_topk_gpu(torch.from_numpy(sc).cuda(), torch.from_numpy(ix).cuda(), parts, k)
+    s, i = s.cpu().numpy(), i.cpu().numpy()
+    for q in range(nq):
+        ok = ix[q] >= 0
+        order = np.lexsort((ix[q][ok], -sc[q][ok]))[:k]
+        assert np.array_equal(i[q], ix[q][ok][order]) and np.array_equal(s[q], sc[q][ok][order])
+
+
+def test_filter_tile_per_block_near_duplicates(monkeypatch):
+    """The filter pass's tile is chosen per query block from that block's sampled candidate counts
+    (no state carried between searches): a near-duplicate block runs gemm_kernel 256 x 256, a random
+    block G2 256 x 192. Two bounded searches of the near-duplicate queries, then random queries,
+    then the near-duplicates again: each equals the full exact scan bit for bit, the second equals
+    the first, and the stats show which tile served which block."""
+    monkeypatch.setenv("CLM_SEARCH_BOUNDED", "1")
+    n, dim, k = 400_000, 128, 5
+    g = torch.Generator(device="cuda").manual_seed(8)
+    rows = torch.randn((n, dim), generator=g, device="cuda")
+    dups = torch.randn((4, dim), generator=g, device="cuda")
+    for j in range(4):
+        rows[j * 90_000: j * 90_000 + 40_000] = dups[j] + 1e-3 * torch.randn((40_000, dim), generator=g,
+                                                                               device="cuda")
+    idx = CosineIndex(dim, capacity=n)
+    idx.append(rows.half())
+    qd = dups.repeat(16, 1).half()
+    qr = torch.randn((64, dim), generator=g, device="cuda").half()
+    runs = [idx.search(qd, k), idx.search(qd, k)]
+    st = idx.stats()
+    assert st["filter_dense"] == 2 * qd.shape[0] and st["filter_g2"] == 0, st
+    runs.append(idx.search(qr, k))
+    st2 = idx.stats()
+    assert st2["filter_g2"] == qr.shape[0] and st2["filter_dense"] == st["filter_dense"], st2
+    runs.append(idx.search(qd, k))
+    monkeypatch.delenv("CLM_SEARCH_BOUNDED")
+    monkeypatch.setenv("CLM_SEARCH_FULL", "1")
+    ref_d, ref_r = idx.search(qd, k), idx.search(qr, k)
+    for (s, i), (rs, ri) in zip(runs, [ref_d, ref_d, ref_r, ref_d]):
+        assert torch.equal(i, ri) and torch.equal(s, rs)
+    idx.close()

@@ -119,6 +119,34 @@ def test_search_oracle_vs_reference_fp32_golden(name, k):
         assert np.median(gaps) < 1e-4
 
 
+@pytest.mark.parametrize("name", ["gauss", "clus"])
+@pytest.mark.parametrize("k", [1025, 2000, 4096])
+def test_search_oracle_vs_reference_large_k(name, k):
+    """k > 1024 up to k = N (search_large_k.npz, the reference's own top_k_similar on the fp32 sets):
+    the oracle's exact ranking equals it up to 2e-6 near-ties, scores to fp32 rounding."""
+    g = golden("search_large_k.npz")
+    gr, gq, cr, cq = syn.fp32_search_inputs()
+    rows, qs = (gr, gq[:4]) if name == "gauss" else (cr, cq[:4])
+    exact = S.cosine_scores(qs, rows)
+    vals, idx = S.topk(exact, k)
+    for q in range(4):
+        assert S.same_topk_up_to_ties(idx[q], g[f"{name}_idx_k{k}"][q].astype(np.int64), exact[q], 2e-6)
+    assert np.max(np.abs(vals - g[f"{name}_vals_k{k}"])) < 1e-6
+
+
+@pytest.mark.parametrize("k", [5, 50, 1500])
+def test_search_oracle_vs_reference_wide_dim(k):
+    """dim 1536 (> 1024) rows through the reference's top_k_similar: the oracle agrees."""
+    g = golden("search_large_k.npz")
+    rows = syn.gaussian_rows(2048, 1536, seed=int(g["wide_seeds"][0]), fp16=False)
+    qs = syn.gaussian_rows(8, 1536, seed=int(g["wide_seeds"][1]), fp16=False)
+    exact = S.cosine_scores(qs, rows)
+    vals, idx = S.topk(exact, k)
+    for q in range(8):
+        assert S.same_topk_up_to_ties(idx[q], g[f"wide_idx_k{k}"][q].astype(np.int64), exact[q], 2e-6)
+    assert np.max(np.abs(vals - g[f"wide_vals_k{k}"])) < 1e-6
+
+
 def test_image_oracle_reproduces_clip_image_processor_golden():
     """oracle.image_ref (PIL's bicubic resample restated + transformers' size / crop rules) gives
     the pixel_values CLIPImageProcessor produced for the reference's 17 committed images and the
