@@ -100,14 +100,19 @@ struct HostTensor {
 
 struct LayerW {
   float *ln1_g = nullptr, *ln1_b = nullptr, *ln2_g = nullptr, *ln2_b = nullptr;
-  u16* w_qkv = nullptr; float* b_qkv = nullptr; int k_qkv = 0;
-  u16* w_out = nullptr; float* b_out = nullptr; int k_out = 0;
-  u16* w_fc1 = nullptr; float* b_fc1 = nullptr; int k_fc1 = 0;
-  u16* w_fc2 = nullptr; float* b_fc2 = nullptr; int k_fc2 = 0;
-  float* a_qkv = nullptr; int r_qkv = 0;   // unmerged LoRA A (fp32) per GEMM input
-  float* a_out = nullptr; int r_out = 0;
-  float* a_fc1 = nullptr; int r_fc1 = 0;
-  float* a_fc2 = nullptr; int r_fc2 = 0;
+  // k_*: the weight's row stride and the K of GEMMs that need whole 64-wide K-steps (G2, split-K);
+  // kl_*: the logical K, in + round_up(r, 32) in unmerged-LoRA mode (gemm_kernel and the fused
+  // attention run the 32-wide last K-step), = k_* otherwise
+  u16* w_qkv = nullptr; float* b_qkv = nullptr; int k_qkv = 0, kl_qkv = 0;
+  u16* w_out = nullptr; float* b_out = nullptr; int k_out = 0, kl_out = 0;
+  u16* w_fc1 = nullptr; float* b_fc1 = nullptr; int k_fc1 = 0, kl_fc1 = 0;
+  u16* w_fc2 = nullptr; float* b_fc2 = nullptr; int k_fc2 = 0, kl_fc2 = 0;
+  // unmerged LoRA: the stacked A of each GEMM input in the compute dtype, [RPAD, in] with zero rows
+  // past r_* (the down-projection GEMM writes all RPAD extension columns: the pad ones get zeros)
+  u16* a_qkv = nullptr; int r_qkv = 0;
+  u16* a_out = nullptr; int r_out = 0;
+  u16* a_fc1 = nullptr; int r_fc1 = 0;
+  u16* a_fc2 = nullptr; int r_fc2 = 0;
 };
 
 struct Tower {
@@ -133,7 +138,10 @@ struct Tower {
   int64_t ldx = 0, ldo = 0, ldm = 0;
 };
 
-constexpr int RPAD = 64;  // K-extension width of the unmerged LoRA mode (K stays a multiple of 64)
+// K-extension width of the unmerged LoRA mode: the storage (weight columns, activation columns;
+// rows stay whole 64-wide K-steps), of which GEMMs multiply round_up(sum r, 32) (LORA_GRANULE)
+constexpr int RPAD = 64;
+constexpr int LORA_GRANULE = 32;
 
 }  // namespace
 
@@ -265,6 +273,14 @@ int upload_16(clm_ctx* c, const std::vector<float>& v, u16** dst, bool bf) {
   return CLM_OK;
 }
 
+// the stacked LoRA A [r_ext, in] (fp32 host) as the [RPAD, in] 16-bit W operand of the
+// down-projection GEMM, rows r_ext .. RPAD-1 zero
+int upload_lora_a(clm_ctx* c, const std::vector<float>& A, int r_ext, int in, u16** dst, bool bf) {
+  std::vector<float> pad((size_t)RPAD * in, 0.f);
+  std::copy(A.begin(), A.begin() + (size_t)r_ext * in, pad.begin());
+  return upload_16(c, pad, dst, bf);
+}
+
 int get_f32(clm_ctx* c, const std::string& n, int64_t numel, float** dst) {
   const HostTensor* t;
   int r = need(c, n, numel, &t);
@@ -284,7 +300,7 @@ struct LinearSpec {
 // merged: W += s * B A.  unmerged: K = in + RPAD, columns [in + off, in + off + r) = s * B.
 // Also returns the stacked A [r_ext, in] for the unmerged mode.
 int build_fused(clm_ctx* c, const std::vector<LinearSpec>& specs, bool q_scale_first, std::vector<float>& W,
-                std::vector<float>& bias, int& K, std::vector<float>& A_stack, int& r_ext) {
+                std::vector<float>& bias, int& K, std::vector<float>& A_stack, int& r_ext, int& K_log) {
   const clm_model_desc& d = c->desc;
   const bool unmerged = d.lora_mode == CLM_LORA_UNMERGED;
   const int in = specs[0].in;
@@ -295,6 +311,7 @@ int build_fused(clm_ctx* c, const std::vector<LinearSpec>& specs, bool q_scale_f
     if (s.lora) r_ext += d.lora_r;
   }
   K = (unmerged && r_ext > 0) ? in + RPAD : in;
+  K_log = (unmerged && r_ext > 0) ? in + (r_ext + LORA_GRANULE - 1) / LORA_GRANULE * LORA_GRANULE : in;
   if (r_ext > RPAD) return fail(CLM_E_ARG, "LoRA rank too large for the K-extension (sum r > 64)");
   W.assign((size_t)total_out * K, 0.f);
   bias.assign(total_out, 0.f);
@@ -371,33 +388,33 @@ int build_tower(clm_ctx* c, Tower& T, bool vision) {
     if ((r = get_f32(c, p + ".layer_norm2.weight", T.d, &Lw.ln2_g))) return r;
     if ((r = get_f32(c, p + ".layer_norm2.bias", T.d, &Lw.ln2_b))) return r;
     std::vector<float> W, b, A;
-    int K, rext;
+    int K, rext, KL;
     // q, k, v share the LN1 output: one fused GEMM
     std::vector<LinearSpec> qkv = {{p + ".self_attn.q_proj", T.d, T.d, (tg & CLM_LORA_Q) != 0},
                                    {p + ".self_attn.k_proj", T.d, T.d, (tg & CLM_LORA_K) != 0},
                                    {p + ".self_attn.v_proj", T.d, T.d, (tg & CLM_LORA_V) != 0}};
-    if ((r = build_fused(c, qkv, true, W, b, K, A, rext))) return r;
+    if ((r = build_fused(c, qkv, true, W, b, K, A, rext, KL))) return r;
     if ((r = upload_16(c, W, &Lw.w_qkv, c->bf16(vision))) || (r = upload_f32(c, b, &Lw.b_qkv))) return r;
-    Lw.k_qkv = K; Lw.r_qkv = rext;
-    if (unmerged && rext && (r = upload_f32(c, A, &Lw.a_qkv))) return r;
+    Lw.k_qkv = K; Lw.kl_qkv = KL; Lw.r_qkv = rext;
+    if (unmerged && rext && (r = upload_lora_a(c, A, rext, T.d, &Lw.a_qkv, c->bf16(vision)))) return r;
 
     std::vector<LinearSpec> outp = {{p + ".self_attn.out_proj", T.d, T.d, (tg & CLM_LORA_OUT) != 0}};
-    if ((r = build_fused(c, outp, false, W, b, K, A, rext))) return r;
+    if ((r = build_fused(c, outp, false, W, b, K, A, rext, KL))) return r;
     if ((r = upload_16(c, W, &Lw.w_out, c->bf16(vision))) || (r = upload_f32(c, b, &Lw.b_out))) return r;
-    Lw.k_out = K; Lw.r_out = rext;
-    if (unmerged && rext && (r = upload_f32(c, A, &Lw.a_out))) return r;
+    Lw.k_out = K; Lw.kl_out = KL; Lw.r_out = rext;
+    if (unmerged && rext && (r = upload_lora_a(c, A, rext, T.d, &Lw.a_out, c->bf16(vision)))) return r;
 
     std::vector<LinearSpec> fc1 = {{p + ".mlp.fc1", T.d, T.mlp, (tg & CLM_LORA_FC1) != 0}};
-    if ((r = build_fused(c, fc1, false, W, b, K, A, rext))) return r;
+    if ((r = build_fused(c, fc1, false, W, b, K, A, rext, KL))) return r;
     if ((r = upload_16(c, W, &Lw.w_fc1, c->bf16(vision))) || (r = upload_f32(c, b, &Lw.b_fc1))) return r;
-    Lw.k_fc1 = K; Lw.r_fc1 = rext;
-    if (unmerged && rext && (r = upload_f32(c, A, &Lw.a_fc1))) return r;
+    Lw.k_fc1 = K; Lw.kl_fc1 = KL; Lw.r_fc1 = rext;
+    if (unmerged && rext && (r = upload_lora_a(c, A, rext, T.d, &Lw.a_fc1, c->bf16(vision)))) return r;
 
     std::vector<LinearSpec> fc2 = {{p + ".mlp.fc2", T.mlp, T.d, (tg & CLM_LORA_FC2) != 0}};
-    if ((r = build_fused(c, fc2, false, W, b, K, A, rext))) return r;
+    if ((r = build_fused(c, fc2, false, W, b, K, A, rext, KL))) return r;
     if ((r = upload_16(c, W, &Lw.w_fc2, c->bf16(vision))) || (r = upload_f32(c, b, &Lw.b_fc2))) return r;
-    Lw.k_fc2 = K; Lw.r_fc2 = rext;
-    if (unmerged && rext && (r = upload_f32(c, A, &Lw.a_fc2))) return r;
+    Lw.k_fc2 = K; Lw.kl_fc2 = KL; Lw.r_fc2 = rext;
+    if (unmerged && rext && (r = upload_lora_a(c, A, rext, T.mlp, &Lw.a_fc2, c->bf16(vision)))) return r;
   }
   // projection, transposed to [d, D] for coalesced reads in pool_project
   {
@@ -506,16 +523,29 @@ struct ProfScope {
     if (e_ != hipSuccess) return fail(CLM_E_HIP, std::string("kernel launch ") + #x + ": " + hipGetErrorString(e_)); \
   } while (0)
 
-// LN into X for a layer's q/k/v GEMM input (A_qkv extension in unmerged mode)
-LnArgs ln_into_x(clm_ctx* c, Tower& T, int64_t M, const float* g, const float* b, const float* loraA, int r_ext,
-                 float* h = nullptr) {
+// LN into X for a layer's q/k/v (or fc1) GEMM input
+LnArgs ln_into_x(clm_ctx* c, Tower& T, int64_t M, const float* g, const float* b, float* h = nullptr) {
   LnArgs a{};
   if (!h) h = T.h;
   a.mode = 0; a.src = h; a.lds = T.d; a.hf = h; a.ldh = T.d;
   a.g1 = g; a.b1 = b; a.y = T.X; a.ldy = T.ldx;
-  a.loraA = loraA; a.r_ext = r_ext; a.r_pad = loraA ? RPAD : 0;
   a.M = (int)M; a.d = T.d; a.eps = c->desc.ln_eps;
   return a;
+}
+
+// Unmerged LoRA, the down-projection of a GEMM input (PEFT lora_A, models/clip_model.py:78):
+// X[:, K : K + RPAD) = X[:, :K] . A^T as a skinny MFMA GEMM (N = RPAD, 128 x 64 tiles, fp32
+// accumulate, rounded once to the compute dtype), so the consumer GEMM's K-extension
+// [X | X A^T] . [W | (alpha/r) B]^T adds the low-rank update in its own main loop. The input's
+// rows are read once more (19.7 MB for the vision q/k/v input at batch 256, ~3 us); the round-4
+// VALU form (24 wave reductions per row inside the LayerNorm / a row-per-wave kernel) cost
+// 1.6 ms per pair step (profiles/r05_v2_unmerged_trace.txt).
+hipError_t lora_down_gemm(bool bf, u16* X, int64_t ldx, int M, int K, const u16* A, const int* mdev,
+                          hipStream_t st) {
+  GemmArgs g{};
+  g.A = X; g.lda = ldx; g.W = A; g.ldw = K; g.M = M; g.N = RPAD; g.K = K;
+  g.out = X + K; g.ldo = ldx; g.m_dev = mdev;
+  return gemm_cfg(bf, EPI_STORE, GEMM_CFG_SPLITK, g, st);
 }
 
 // Last-layer pruning (default; $CLM_NO_PRUNE=1 runs every row): the encoders return only the
@@ -538,7 +568,7 @@ bool prune_last_layer() {
 // output. Only each caption's live rows (through its first EOS) are packed and encoded; the
 // embeddings are bit-identical to encoding all L rows (rows are independent in every kernel but
 // attention, whose keys of a live query are all live; tests/test_gpu_encode.py). Needs the fused
-// attention kernel and no unmerged-LoRA K-extension.
+// attention kernel (unmerged LoRA included: its down-projection GEMMs read the live row count too).
 bool text_varlen_enabled() {
   static int v = -1;
   if (v < 0) {
@@ -589,14 +619,14 @@ int make_run(clm_ctx* c, Tower& T, int B, int S, bool causal, const int32_t* ids
 AttnProblem attn_problem(const LayerRun& R, int l) {
   Tower& T = *R.T;
   const LayerW& Lw = T.layers[l];
-  AttnProblem p{T.X, T.ldx, Lw.w_qkv, Lw.k_qkv, Lw.b_qkv, T.O, T.ldo, R.B, R.S, T.H, T.d, Lw.k_qkv,
+  AttnProblem p{T.X, T.ldx, Lw.w_qkv, Lw.k_qkv, Lw.b_qkv, T.O, T.ldo, R.B, R.S, T.H, T.d, Lw.kl_qkv,
                 nullptr, nullptr, nullptr, nullptr};
   if (R.vl) { p.lens = T.vl_lens; p.offs = T.vl_offs; p.tiles = T.vl_tiles; p.counts = T.vl_counts; }
   return p;
 }
 double attn_flops(const LayerRun& R, int l) {
   const Tower& T = *R.T;
-  return 2.0 * R.Mx * 3 * T.d * T.layers[l].k_qkv + 4.0 * T.H * R.attn_pairs * 64;
+  return 2.0 * R.Mx * 3 * T.d * T.layers[l].kl_qkv + 4.0 * T.H * R.attn_pairs * 64;
 }
 
 // layer l's q/k/v projection + attention of one tower: T.X -> T.O
@@ -605,7 +635,7 @@ int attn_step(clm_ctx* c, const LayerRun& R, int l, hipStream_t st) {
   LayerW& Lw = T.layers[l];
   const bool bf = R.bf;
   GemmArgs g{};
-  g.A = T.X; g.lda = T.ldx; g.M = R.B * R.S; g.N = 3 * T.d; g.K = Lw.k_qkv; g.out = T.QKV; g.ldo = 3 * T.d;
+  g.A = T.X; g.lda = T.ldx; g.M = R.B * R.S; g.N = 3 * T.d; g.K = Lw.kl_qkv; g.out = T.QKV; g.ldo = 3 * T.d;
   g.W = Lw.w_qkv; g.ldw = Lw.k_qkv; g.bias = Lw.b_qkv;
   if (R.vl) {   // packed live rows of variable-length captions
     PROF(CLM_PROF_GEMM, attn_flops(R, l));
@@ -653,20 +683,22 @@ PostOps post_ops(clm_ctx* c, const LayerRun& R, int l, int64_t M, float* h, u16*
   PostOps p{};
   p.rows = pooled ? (double)M : R.Mx;
   GemmArgs& g = p.out;
-  g.A = O; g.lda = T.ldo; g.W = Lw.w_out; g.ldw = Lw.k_out; g.M = (int)M; g.N = T.d; g.K = Lw.k_out;
+  // pooled rows: split-K over whole 64-wide K-steps (the extension's pad columns are zero on both sides)
+  g.A = O; g.lda = T.ldo; g.W = Lw.w_out; g.ldw = Lw.k_out; g.M = (int)M; g.N = T.d; g.K = pooled ? Lw.k_out : Lw.kl_out;
   g.out = h; g.ldo = T.d; g.bias = Lw.b_out; g.m_dev = mdev;
-  p.ln2 = ln_into_x(c, T, M, Lw.ln2_g, Lw.ln2_b, Lw.a_fc1, Lw.r_fc1, h);
+  p.ln2 = ln_into_x(c, T, M, Lw.ln2_g, Lw.ln2_b, h);
   p.ln2.m_dev = mdev;
   GemmArgs& f = p.fc1;
   f.A = T.X; f.lda = T.ldx; f.M = (int)M; f.N = T.mlp; f.K = Lw.k_fc1; f.out = T.Hm; f.ldo = T.ldm;
   f.W = Lw.w_fc1; f.ldw = Lw.k_fc1; f.bias = Lw.b_fc1; f.m_dev = mdev;
   GemmArgs& f2 = p.fc2;
-  f2.A = T.Hm; f2.lda = T.ldm; f2.W = Lw.w_fc2; f2.ldw = Lw.k_fc2; f2.M = (int)M; f2.N = T.d; f2.K = Lw.k_fc2;
+  f2.A = T.Hm; f2.lda = T.ldm; f2.W = Lw.w_fc2; f2.ldw = Lw.k_fc2; f2.M = (int)M; f2.N = T.d;
+  f2.K = pooled ? Lw.k_fc2 : Lw.kl_fc2;
   f2.out = h; f2.ldo = T.d; f2.bias = Lw.b_fc2; f2.m_dev = mdev;
   p.has_ln1 = l + 1 < T.L;
   if (p.has_ln1) {
     LayerW& Ln = T.layers[l + 1];
-    p.ln1 = ln_into_x(c, T, M, Ln.ln1_g, Ln.ln1_b, Ln.a_qkv, Ln.r_qkv);
+    p.ln1 = ln_into_x(c, T, M, Ln.ln1_g, Ln.ln1_b);
     p.ln1.m_dev = mdev;
   }
   return p;
@@ -692,8 +724,9 @@ int post_attn_step(clm_ctx* c, const LayerRun& R, int l, bool* pooled_rows, hipS
     *pooled_rows = true;
   }
   PostOps p = post_ops(c, R, l, M, h, O, pooled);
-  if (Lw.r_out) { PROF(CLM_PROF_OTHER, 2.0 * M * T.d + 4.0 * Lw.r_out * T.d);
-    KCHK(lora_down(bf, O, T.ldo, (int)M, T.d, Lw.a_out, Lw.r_out, RPAD, st)); }
+  const int* mdev = pooled ? nullptr : R.mdev;
+  if (Lw.r_out) { PROF(CLM_PROF_GEMM, 2.0 * p.rows * RPAD * T.d);
+    KCHK(lora_down_gemm(bf, O, T.ldo, (int)M, T.d, Lw.a_out, mdev, st)); }
   if (pooled) {
     int r = pooled_resid(c, R, p.out, st);
     if (r) return r;
@@ -701,17 +734,24 @@ int post_attn_step(clm_ctx* c, const LayerRun& R, int l, bool* pooled_rows, hipS
     PROF(CLM_PROF_GEMM, 2.0 * p.rows * p.out.N * p.out.K); KCHK(gemm(bf, EPI_RESID, p.out, st));
   }
   { PROF(CLM_PROF_LN, p.rows * T.d * 6.0); KCHK(layernorm(bf, p.ln2, st)); }
+  if (Lw.r_fc1) { PROF(CLM_PROF_GEMM, 2.0 * p.rows * RPAD * T.d);
+    KCHK(lora_down_gemm(bf, T.X, T.ldx, (int)M, T.d, Lw.a_fc1, mdev, st)); }
   { PROF(CLM_PROF_GEMM, 2.0 * p.rows * p.fc1.N * p.fc1.K);   // pooled rows: 128 x 64 tiles (4 waves) fill the chip
     KCHK(pooled ? gemm_cfg(bf, EPI_GELU, GEMM_CFG_SPLITK, p.fc1, st) : gemm(bf, EPI_GELU, p.fc1, st)); }
-  if (Lw.r_fc2) { PROF(CLM_PROF_OTHER, 2.0 * M * T.mlp + 4.0 * Lw.r_fc2 * T.mlp);
-    KCHK(lora_down(bf, T.Hm, T.ldm, (int)M, T.mlp, Lw.a_fc2, Lw.r_fc2, RPAD, st)); }
+  if (Lw.r_fc2) { PROF(CLM_PROF_GEMM, 2.0 * p.rows * RPAD * T.mlp);
+    KCHK(lora_down_gemm(bf, T.Hm, T.ldm, (int)M, T.mlp, Lw.a_fc2, mdev, st)); }
   if (pooled) {
     int r = pooled_resid(c, R, p.fc2, st);
     if (r) return r;
   } else {
     PROF(CLM_PROF_GEMM, 2.0 * p.rows * p.fc2.N * p.fc2.K); KCHK(gemm(bf, EPI_RESID, p.fc2, st));
   }
-  if (p.has_ln1) { PROF(CLM_PROF_LN, p.rows * T.d * 6.0); KCHK(layernorm(bf, p.ln1, st)); }
+  if (p.has_ln1) {
+    { PROF(CLM_PROF_LN, p.rows * T.d * 6.0); KCHK(layernorm(bf, p.ln1, st)); }
+    const LayerW& Ln = T.layers[l + 1];
+    if (Ln.r_qkv) { PROF(CLM_PROF_GEMM, 2.0 * p.rows * RPAD * T.d);
+      KCHK(lora_down_gemm(bf, T.X, T.ldx, (int)M, T.d, Ln.a_qkv, mdev, st)); }
+  }
   return CLM_OK;
 }
 
@@ -777,20 +817,25 @@ int run_layers_pair(clm_ctx* c, const LayerRun& V, const LayerRun& X, hipStream_
     PostOps pv = post_ops(c, V, l, (int64_t)V.B * V.S, TV.h, TV.O, false);
     PostOps px = post_ops(c, X, l, (int64_t)X.B * X.S, TX.h, TX.O, false);
     const LayerW &Lv = TV.layers[l], &Lx = TX.layers[l];
-    if (Lv.r_out) KCHK(lora_down(V.bf, TV.O, TV.ldo, pv.out.M, TV.d, Lv.a_out, Lv.r_out, RPAD, st));
-    if (Lx.r_out) KCHK(lora_down(X.bf, TX.O, TX.ldo, px.out.M, TX.d, Lx.a_out, Lx.r_out, RPAD, st));
+    if (Lv.r_out) KCHK(lora_down_gemm(V.bf, TV.O, TV.ldo, pv.out.M, TV.d, Lv.a_out, V.mdev, st));
+    if (Lx.r_out) KCHK(lora_down_gemm(X.bf, TX.O, TX.ldo, px.out.M, TX.d, Lx.a_out, X.mdev, st));
     { PROF(CLM_PROF_GEMM, 2.0 * (pv.rows * pv.out.N * pv.out.K + px.rows * px.out.N * px.out.K));
       KCHK(gemm_pair(V.bf, X.bf, EPI_RESID, -1, pv.out, px.out, pair_persist(), st)); }
     { PROF(CLM_PROF_LN, (pv.rows * TV.d + px.rows * TX.d) * 6.0);
       KCHK(layernorm_pair(V.bf, X.bf, pv.ln2, px.ln2, st)); }
+    if (Lv.r_fc1) KCHK(lora_down_gemm(V.bf, TV.X, TV.ldx, pv.fc1.M, TV.d, Lv.a_fc1, V.mdev, st));
+    if (Lx.r_fc1) KCHK(lora_down_gemm(X.bf, TX.X, TX.ldx, px.fc1.M, TX.d, Lx.a_fc1, X.mdev, st));
     { PROF(CLM_PROF_GEMM, 2.0 * (pv.rows * pv.fc1.N * pv.fc1.K + px.rows * px.fc1.N * px.fc1.K));
       KCHK(gemm_pair(V.bf, X.bf, EPI_GELU, -1, pv.fc1, px.fc1, pair_persist(), st)); }
-    if (Lv.r_fc2) KCHK(lora_down(V.bf, TV.Hm, TV.ldm, pv.fc2.M, TV.mlp, Lv.a_fc2, Lv.r_fc2, RPAD, st));
-    if (Lx.r_fc2) KCHK(lora_down(X.bf, TX.Hm, TX.ldm, px.fc2.M, TX.mlp, Lx.a_fc2, Lx.r_fc2, RPAD, st));
+    if (Lv.r_fc2) KCHK(lora_down_gemm(V.bf, TV.Hm, TV.ldm, pv.fc2.M, TV.mlp, Lv.a_fc2, V.mdev, st));
+    if (Lx.r_fc2) KCHK(lora_down_gemm(X.bf, TX.Hm, TX.ldm, px.fc2.M, TX.mlp, Lx.a_fc2, X.mdev, st));
     { PROF(CLM_PROF_GEMM, 2.0 * (pv.rows * pv.fc2.N * pv.fc2.K + px.rows * px.fc2.N * px.fc2.K));
       KCHK(gemm_pair(V.bf, X.bf, EPI_RESID, -1, pv.fc2, px.fc2, pair_persist(), st)); }
     { PROF(CLM_PROF_LN, (pv.rows * TV.d + px.rows * TX.d) * 6.0);
       KCHK(layernorm_pair(V.bf, X.bf, pv.ln1, px.ln1, st)); }
+    const LayerW &Nv = TV.layers[l + 1], &Nx = TX.layers[l + 1];
+    if (Nv.r_qkv) KCHK(lora_down_gemm(V.bf, TV.X, TV.ldx, pv.fc1.M, TV.d, Nv.a_qkv, V.mdev, st));
+    if (Nx.r_qkv) KCHK(lora_down_gemm(X.bf, TX.X, TX.ldx, px.fc1.M, TX.d, Nx.a_qkv, X.mdev, st));
   }
   return CLM_OK;
 }
@@ -822,9 +867,11 @@ int image_prologue(clm_ctx* c, Tower& T, const void* pix, int layout, int B, hip
   g.out = T.h; g.ldo = T.d; g.aux = T.pos; g.aux_ld = T.d; g.group = G * G;
   { PROF(CLM_PROF_GEMM, 2.0 * g.M * g.N * g.K); KCHK(gemm(bf, EPI_PATCH, g, st)); }
   { PROF(CLM_PROF_OTHER, (double)B * T.d * 4.0); KCHK(write_cls(T.h, T.d, B, Tn, T.d, T.cls, T.pos, st)); }
-  LnArgs a = ln_into_x(c, T, (int64_t)B * Tn, T.pre_g, T.pre_b, T.layers[0].a_qkv, T.layers[0].r_qkv);
+  LnArgs a = ln_into_x(c, T, (int64_t)B * Tn, T.pre_g, T.pre_b);
   a.g2 = T.layers[0].ln1_g; a.b2 = T.layers[0].ln1_b;  // pre_layrnorm (in place) then layer-0 LN1
   { PROF(CLM_PROF_LN, (double)B * Tn * T.d * 10.0); KCHK(layernorm(bf, a, st)); }
+  if (T.layers[0].r_qkv) { PROF(CLM_PROF_GEMM, 2.0 * B * Tn * RPAD * T.d);
+    KCHK(lora_down_gemm(bf, T.X, T.ldx, B * Tn, T.d, T.layers[0].a_qkv, nullptr, st)); }
   return CLM_OK;
 }
 
@@ -858,11 +905,9 @@ int text_prologue(clm_ctx* c, Tower& T, const int32_t* ids_dev, int B, int L, bo
   LnArgs a{};
   a.mode = 1; a.ids = ids_dev; a.tok = T.tok; a.pos = T.tpos; a.L = L;
   a.hf = T.h; a.ldh = T.d; a.g1 = T.layers[0].ln1_g; a.b1 = T.layers[0].ln1_b;
-  a.y = T.X; a.ldy = T.ldx; a.loraA = T.layers[0].a_qkv; a.r_ext = T.layers[0].r_qkv;
-  a.r_pad = a.loraA ? RPAD : 0; a.M = B * L; a.d = T.d; a.eps = d.ln_eps;
+  a.y = T.X; a.ldy = T.ldx; a.M = B * L; a.d = T.d; a.eps = d.ln_eps;
   bool vl = text_varlen_enabled() && T.vl_lens && B <= 4096 &&   // text_plan: <= 4096 captions per chunk
             fused_attention(L, T.H, T.d, T.layers.empty() ? 0 : T.layers[0].k_qkv);
-  for (const LayerW& Lw : T.layers) vl = vl && !Lw.r_qkv && !Lw.r_out && !Lw.r_fc1 && !Lw.r_fc2;
   if (vl) {
     { PROF(CLM_PROF_OTHER, (double)B * L * 8.0);
       KCHK(text_plan(ids_dev, B, L, d.eos_token_id, T.vl_lens, T.vl_offs, T.vl_rowmap, T.vl_tiles, T.vl_counts, st)); }
@@ -871,6 +916,8 @@ int text_prologue(clm_ctx* c, Tower& T, const int32_t* ids_dev, int B, int L, bo
   }
   *vl_out = vl;
   { PROF(CLM_PROF_LN, (double)B * L * T.d * 14.0); KCHK(layernorm(bf, a, st)); }
+  if (T.layers[0].r_qkv) { PROF(CLM_PROF_GEMM, 2.0 * B * L * RPAD * T.d);
+    KCHK(lora_down_gemm(bf, T.X, T.ldx, B * L, T.d, T.layers[0].a_qkv, vl ? T.vl_counts : nullptr, st)); }
   return CLM_OK;
 }
 

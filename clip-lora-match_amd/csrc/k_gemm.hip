@@ -51,7 +51,10 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& ga, int bid, int G) {
   const TileWalk tw = tile_walk(ntiles, bid, G);
   if (tw.count <= 0) return;   // varlen: fewer live tiles than the grid
   const int n_my = tw.count;
-  const int nk = g.K / BK / ks;
+  // K % 64 == 32 (unmerged LoRA's 32-wide K-extension granule): the last K-step's DMA still moves
+  // 64 columns (operand rows are readable to round_up(K, 64)) but only its first 32 are multiplied
+  const int nk = (g.K + BK - 1) / BK / ks;
+  const bool half_last = (g.K % BK) != 0;
   const int S = n_my * nk;   // K-steps of all this workgroup's tiles, one ring
 
   auto coords = [&](int i, int& m0, int& n0, int& k0) {
@@ -175,6 +178,7 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& ga, int bid, int G) {
     const uint8_t* sb = sa + BM * 128;
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
+      if (kk == 1 && half_last && c_kt == nk - 1) break;
       const int c = kk * 4 + (lane >> 4);
       u32x4 af[C::TM], bw[C::TN];
 #pragma unroll
@@ -374,8 +378,15 @@ int gemm_num_configs() { return NCFG; }
 
 hipError_t gemm_cfg(bool bf16, int epi, int config, const GemmArgs& g, hipStream_t s) {
   if (g.M <= 0 || g.N <= 0) return hipSuccess;
-  if (g.K <= 0 || (g.K % BK) != 0 || (g.lda % 8) != 0 || (g.ldw % 8) != 0) return hipErrorInvalidValue;
-  const int id = config >= 0 ? config : pick_config(epi, g.M, g.N);
+  if (g.K <= 0 || (g.K % 32) != 0 || (g.lda % 8) != 0 || (g.ldw % 8) != 0) return hipErrorInvalidValue;
+  int id = config >= 0 ? config : pick_config(epi, g.M, g.N);
+  if (g.K % BK) {   // the half last K-step: gemm_kernel configs without split-K only
+    if (g.ksplit > 1) return hipErrorInvalidValue;
+    if (id >= 8) {
+      if (config >= 0) return hipErrorInvalidValue;
+      id = pick_from(MODELS, g.M, g.N);
+    }
+  }
   return bf16 ? dispatch<true>(epi, id, g, s) : dispatch<false>(epi, id, g, s);
 }
 
@@ -553,9 +564,13 @@ hipError_t gemm_pair(bool bf0, bool bf1, int epi, int config, const GemmArgs& g0
   if (g0.M <= 0 || g0.N <= 0) return gemm(bf1, epi, g1, s);
   if (g1.M <= 0 || g1.N <= 0) return gemm(bf0, epi, g0, s);
   for (const GemmArgs* g : {&g0, &g1})
-    if (g->K <= 0 || (g->K % BK) != 0 || (g->lda % 8) != 0 || (g->ldw % 8) != 0 || g->ksplit > 1)
+    if (g->K <= 0 || (g->K % 32) != 0 || (g->lda % 8) != 0 || (g->ldw % 8) != 0 || g->ksplit > 1)
       return hipErrorInvalidValue;
   const int id = config >= 0 ? config : pick_pair_config(epi, g0, g1);
+  if (id >= 8 && ((g0.K % BK) || (g1.K % BK))) {   // G2 needs whole K-steps: two launches
+    hipError_t e = gemm(bf0, epi, g0, s);
+    return e != hipSuccess ? e : gemm(bf1, epi, g1, s);
+  }
   if (bf0 && !bf1) return pair_by_epi<true, false>(epi, id, g0, g1, persist, s);
   if (bf0 == bf1) return bf0 ? pair_by_epi<true, true>(epi, id, g0, g1, persist, s)
                              : pair_by_epi<false, false>(epi, id, g0, g1, persist, s);

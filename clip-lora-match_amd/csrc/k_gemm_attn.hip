@@ -88,7 +88,8 @@ __device__ __forceinline__ void gemm_attn_body(const FaArgs& a, int bid, int nwg
     M = (int64_t)a.B * a.T;
   }
   const int h = t % a.H;
-  const int nk = a.K / BK;
+  const int nk = (a.K + BK - 1) / BK;   // K % 64 == 32: the last step multiplies its first 32 columns
+  const bool half_last = (a.K % BK) != 0;
 
   // ---- main loop: acc[256 x 192] = X[m0 .. m0 + 255, :] . W[head h's q, k, v rows]^T --------
   const int r8 = lane >> 3, pc = lane & 7;
@@ -141,6 +142,7 @@ __device__ __forceinline__ void gemm_attn_body(const FaArgs& a, int bid, int nwg
     const uint8_t* sb = sa + FA_BM * 128;
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
+      if (kk == 1 && half_last && s == nk - 1) break;
       const int c = kk * 4 + g;
       u32x4 af[FA_TM], bw[FA_TN];
 #pragma unroll
@@ -324,7 +326,7 @@ hipError_t launch(const FaArgs& a, int tiles, hipStream_t s) {
 }  // namespace
 
 bool gemm_attn_supported(int T, int H, int d, int K) {
-  return T >= 1 && T <= 128 && d == H * 64 && K > 0 && K % BK == 0;
+  return T >= 1 && T <= 128 && d == H * 64 && K > 0 && K % 32 == 0;
 }
 
 namespace {

@@ -86,21 +86,6 @@ __global__ __launch_bounds__(256) void ln_kernel(LnArgs aa) {
 #pragma unroll
   for (int i = 0; i < NP; ++i) *(uint32_t*)(y + (i * 64 + lane) * 2) = pack2<BF>(x[i][0], x[i][1]);
 
-  if (a.loraA) {  // y[:, d + j] = sum_e x_e * A[j, e]
-    float mine = 0.f;
-    for (int j = 0; j < a.r_ext; ++j) {
-      const float* A = a.loraA + (int64_t)j * d;
-      float s = 0.f;
-#pragma unroll
-      for (int i = 0; i < NP; ++i) {
-        const float2 w = *(const float2*)(A + (i * 64 + lane) * 2);
-        s += x[i][0] * w.x + x[i][1] * w.y;
-      }
-      s = wave_sum(s);
-      if (lane == j) mine = s;
-    }
-    if (lane < a.r_pad) y[d + lane] = from_f32<BF>(lane < a.r_ext ? mine : 0.f);
-  }
 }
 
 // d % 256 == 0: lane owns NQ float4 at e = (i*64 + lane)*4 (16-B loads, 8-B bf16 stores: half
@@ -183,7 +168,7 @@ __device__ __forceinline__ void ln4_body(const LnArgs& aa, int bid) {
     if (a.mode == 1) store_h();
     ln(a.g1, a.b1);
   }
-  if (!a.loraA && row0 + R - 1 < a.M && (a.ldy % 8) == 0) {
+  if (row0 + R - 1 < a.M && (a.ldy % 8) == 0) {
     // 16-B stores for each pair of the wave's rows: lane pairs (2l, 2l+1) swap one 8-B half by
     // DPP, then the even lane stores row 0's 8 consecutive values, the odd lane row 1's (one
     // store instruction per chunk for both rows instead of two 8-B ones; same values)
@@ -212,21 +197,6 @@ __device__ __forceinline__ void ln4_body(const LnArgs& aa, int bid) {
 #pragma unroll
     for (int i = 0; i < NQ; ++i)
       *(u32x2*)(y + (i * 64 + lane) * 4) = u32x2{pack2<BF>(x[r][i].x, x[r][i].y), pack2<BF>(x[r][i].z, x[r][i].w)};
-    if (a.loraA) {  // y[:, d + j] = sum_e x_e * A[j, e]
-      float mine = 0.f;
-      for (int j = 0; j < a.r_ext; ++j) {
-        const float* A = a.loraA + (int64_t)j * d;
-        float sj = 0.f;
-#pragma unroll
-        for (int i = 0; i < NQ; ++i) {
-          const float4 w = *(const float4*)(A + (i * 64 + lane) * 4);
-          sj += (x[r][i].x * w.x + x[r][i].y * w.y) + (x[r][i].z * w.z + x[r][i].w * w.w);
-        }
-        sj = wave_sum(sj);
-        if (lane == j) mine = sj;
-      }
-      if (lane < a.r_pad) y[d + lane] = from_f32<BF>(lane < a.r_ext ? mine : 0.f);
-    }
   }
 }
 
@@ -268,29 +238,6 @@ hipError_t ln_dispatch(const LnArgs& a, hipStream_t s) {
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();
-}
-
-// -------------------------------------------------------------- lora_down --
-template <bool BF>
-__global__ __launch_bounds__(256) void lora_down_kernel(u16* X, int64_t ldx, int M, int K,
-                                                        const float* A, int r_ext, int r_pad) {
-  const int lane = threadIdx.x & 63;
-  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (row >= M) return;
-  u16* x = X + (int64_t)row * ldx;
-  float mine = 0.f;
-  for (int j = 0; j < r_ext; ++j) {
-    const float* a = A + (int64_t)j * K;
-    float s = 0.f;
-    for (int e = lane * 2; e < K; e += 128) {
-      const uint32_t pr = *(const uint32_t*)(x + e);
-      const float2 w = *(const float2*)(a + e);
-      s += to_f32<BF>((u16)(pr & 0xffff)) * w.x + to_f32<BF>((u16)(pr >> 16)) * w.y;
-    }
-    s = wave_sum(s);
-    if (lane == j) mine = s;
-  }
-  if (lane < r_pad) x[K + lane] = from_f32<BF>(lane < r_ext ? mine : 0.f);
 }
 
 // -------------------------------------------------------------- patchify ---
@@ -699,14 +646,12 @@ __global__ __launch_bounds__(256) void f32_to_f16_kernel(const float* src, int64
 
 hipError_t layernorm(bool bf16, const LnArgs& a, hipStream_t s) {
   if (a.M <= 0) return hipSuccess;
-  if (a.r_ext > 64 || a.r_pad > 64) return hipErrorInvalidValue;
   return bf16 ? ln_dispatch<true>(a, s) : ln_dispatch<false>(a, s);
 }
 
 hipError_t layernorm_pair(bool bf0, bool bf1, const LnArgs& a0, const LnArgs& a1, hipStream_t s) {
   if (a0.M <= 0) return layernorm(bf1, a1, s);
   if (a1.M <= 0) return layernorm(bf0, a0, s);
-  if (a0.r_ext > 64 || a0.r_pad > 64 || a1.r_ext > 64 || a1.r_pad > 64) return hipErrorInvalidValue;
   hipError_t e = hipErrorNotSupported;
   if (bf0 && !bf1) e = ln_pair_dims<true, false>(a0, a1, s);
   else if (bf0 && bf1) e = ln_pair_dims<true, true>(a0, a1, s);
@@ -716,15 +661,6 @@ hipError_t layernorm_pair(bool bf0, bool bf1, const LnArgs& a0, const LnArgs& a1
   return e != hipSuccess ? e : layernorm(bf1, a1, s);
 }
 
-hipError_t lora_down(bool bf16, u16* X, int64_t ldx, int M, int K, const float* A, int r_ext, int r_pad,
-                     hipStream_t s) {
-  if (M <= 0) return hipSuccess;
-  if (r_ext > 64 || r_pad > 64 || (K % 2)) return hipErrorInvalidValue;
-  dim3 grid((M + 3) / 4), block(256);
-  if (bf16) lora_down_kernel<true><<<grid, block, 0, s>>>(X, ldx, M, K, A, r_ext, r_pad);
-  else lora_down_kernel<false><<<grid, block, 0, s>>>(X, ldx, M, K, A, r_ext, r_pad);
-  return hipGetLastError();
-}
 
 hipError_t patchify(bool bf16, const void* pix, int layout, int B, int S, int p, int C, const float* lut,
                     u16* P, int Kp, hipStream_t s) {

@@ -6,7 +6,9 @@ namespace clm {
 
 // ---------------------------------------------------------------- GEMM ------
 // C[M,N] = A[M,K] . W[N,K]^T  (both operands K-contiguous, nn.Linear layout),
-// bf16 or fp16 operands, fp32 accumulate, fused epilogue. K % 64 == 0.
+// bf16 or fp16 operands, fp32 accumulate, fused epilogue. K % 64 == 0, or K % 64 == 32 (gemm_kernel
+// configs 0-7 without split-K, and gemm_attn): every operand row must then be readable (and finite)
+// to round_up(K, 64) -- the last K-step's DMA moves 64 columns, its MFMAs use the first 32.
 enum Epi {
   EPI_STORE = 0,  // out16[m,n] = acc + bias[n]
   EPI_GELU = 1,   // out16[m,n] = quick_gelu(acc + bias[n])
@@ -81,8 +83,7 @@ int pick_pair_config(int epi, const GemmArgs& g0, const GemmArgs& g1);
 //   mode 1: x = tok[ids[r]] + pos[r % L]         (text embedding gather), h written
 // If g2 != null: h_out = LN(x; g1,b1) is written to hf (fp32) and y = LN(h_out; g2,b2)
 // else: (mode 1 writes hf = x) y = LN(x; g1,b1).
-// y (compute dtype) gets row stride ldy; if loraA != null, the r_ext LoRA
-// down-projections of the fp32 LN output are appended at y[:, d : d+r_pad).
+// y (compute dtype) gets row stride ldy.
 struct LnArgs {
   int mode;
   const float* src; int64_t lds;       // mode 0 source rows
@@ -91,7 +92,6 @@ struct LnArgs {
   const float* g1; const float* b1;
   const float* g2; const float* b2;
   u16* y; int64_t ldy;
-  const float* loraA; int r_ext; int r_pad;   // [r_ext, d] fp32
   int M, d; float eps;
   // varlen rows (packed text tower): rows r < *m_dev only (M sizes the grid); mode 1 reads token
   // rowmap[r] = b * L + position of the padded [B, L] ids instead of r
@@ -101,11 +101,6 @@ hipError_t layernorm(bool bf16, const LnArgs& a, hipStream_t s);
 // the image and text towers' LayerNorms of one layer in one launch (d0 / d1 = 768 / 512 or
 // 1024 / 768; other widths run as two launches), rows bit-identical to layernorm()
 hipError_t layernorm_pair(bool bf0, bool bf1, const LnArgs& a0, const LnArgs& a1, hipStream_t s);
-
-// y[:, K : K+r_pad) = (X[:, :K] . A^T) for LoRA K-extension of a GEMM whose input
-// is not a LayerNorm output (out_proj after attention, fc2 after GELU).
-hipError_t lora_down(bool bf16, u16* X, int64_t ldx, int M, int K, const float* A, int r_ext,
-                     int r_pad, hipStream_t s);
 
 // shortest-edge bicubic resize + centre crop (k_image.hip), PIL / CLIPImageProcessor arithmetic.
 // Per image: source HWC RGB bytes at src + src_off (row stride 3 W); the crop needs source rows

@@ -275,8 +275,10 @@ def test_fused_qkv_attention_bit_identical(preset, dtype, mode):
         assert torch.equal(a, b), f"case {i}: fused vs two-kernel max diff {(a - b).abs().max().item():.3e}"
 
 
-@pytest.mark.parametrize("preset,dtype", [("tiny", "float16"), ("ViT-B/32", "bfloat16"), ("ViT-B/32", "float16")])
-def test_text_varlen_bit_identical(preset, dtype):
+@pytest.mark.parametrize("preset,dtype,mode", [("tiny", "float16", "merged"), ("ViT-B/32", "bfloat16", "merged"),
+                                               ("ViT-B/32", "float16", "merged"), ("tiny", "bfloat16", "unmerged"),
+                                               ("ViT-B/32", "mixed", "unmerged")])
+def test_text_varlen_bit_identical(preset, dtype, mode):
     """Varlen text (default): only each caption's live rows -- through its first EOS, the pooled
     row; the tower is causal, so no later row reaches it -- are packed and encoded (text_plan +
     gemm_attn_varlen + row-count-from-device GEMMs / LayerNorms). The embeddings must equal the
@@ -284,7 +286,7 @@ def test_text_varlen_bit_identical(preset, dtype):
     EOS (pools row 0: one live row), captions filling all L rows, pruned and every-row last layer
     (bit 8), and the two-stream / graph-replayed pair encode with sub-batches."""
     from clip_lora_match_amd import _capi as C
-    m, cfg, sd, lora = _model(preset, dtype, max_batch=64)
+    m, cfg, sd, lora = _model(preset, dtype, mode, max_batch=64)
     ids = syn.captions(61, cfg.max_pos, cfg.bos_token_id, cfg.eos_token_id, 77, min_len=2)
     ids[3] = np.arange(cfg.max_pos) + 5           # no EOS at all
     ids[4, :] = 7
