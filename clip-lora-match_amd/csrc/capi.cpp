@@ -534,7 +534,7 @@ LnArgs ln_into_x(clm_ctx* c, Tower& T, int64_t M, const float* g, const float* b
 }
 
 // Unmerged LoRA, the down-projection of a GEMM input (PEFT lora_A, models/clip_model.py:78):
-// X[:, K : K + RPAD) = X[:, :K] . A^T as a skinny MFMA GEMM (N = RPAD, 128 x 64 tiles, fp32
+// X[:, K : K + RPAD) = X[:, :K] . A^T as a skinny MFMA GEMM (N = RPAD, 64 x 64 tiles, fp32
 // accumulate, rounded once to the compute dtype), so the consumer GEMM's K-extension
 // [X | X A^T] . [W | (alpha/r) B]^T adds the low-rank update in its own main loop. The input's
 // rows are read once more (19.7 MB for the vision q/k/v input at batch 256, ~3 us); the round-4
@@ -545,7 +545,8 @@ hipError_t lora_down_gemm(bool bf, u16* X, int64_t ldx, int M, int K, const u16*
   GemmArgs g{};
   g.A = X; g.lda = ldx; g.W = A; g.ldw = K; g.M = M; g.N = RPAD; g.K = K;
   g.out = X + K; g.ldo = ldx; g.m_dev = mdev;
-  return gemm_cfg(bf, EPI_STORE, GEMM_CFG_SPLITK, g, st);
+  static const int cfg = getenv("CLM_LORA_DOWN_CFG") ? atoi(getenv("CLM_LORA_DOWN_CFG")) : GEMM_CFG_SKINNY;   // A/B
+  return gemm_cfg(bf, EPI_STORE, cfg, g, st);
 }
 
 // Last-layer pruning (default; $CLM_NO_PRUNE=1 runs every row): the encoders return only the
@@ -966,7 +967,10 @@ int clm_gemm(int hip_device, int dtype, int epilogue, int config, const void* A,
   if (epilogue != EPI_STORE && epilogue != EPI_GELU && epilogue != EPI_RESID && epilogue != EPI_SCORE)
     return fail(CLM_E_ARG, "bad epilogue");
   if (config >= gemm_num_configs()) return fail(CLM_E_ARG, "bad config");
-  if (M < 0 || N < 0 || K <= 0 || K % 64) return fail(CLM_E_ARG, "bad shape (K % 64 == 0)");
+  // K % 64 == 32 (the unmerged-LoRA granule): rows must be readable to round_up(K, 64)
+  const int64_t kr = (K + 63) / 64 * 64;
+  if (M < 0 || N < 0 || K <= 0 || K % 32 || (K % 64 && (lda < kr || ldw < kr)))
+    return fail(CLM_E_ARG, "bad shape (K % 64 == 0, or K % 64 == 32 with lda, ldw >= round_up(K, 64))");
   DeviceGuard g(hip_device);
   GemmArgs a{};
   a.A = (const u16*)A; a.lda = lda; a.W = (const u16*)W; a.ldw = ldw; a.M = M; a.N = N; a.K = K;

@@ -286,11 +286,13 @@ hipError_t launch_id(int id, const GemmArgs& g, hipStream_t s) {
     case 6: return launch_cfg<BF, EPI, 128, 256, 2, 4, 2>(g, s);
     case 7: return launch_cfg<BF, EPI, 160, 128, 2, 2, 2>(g, s);
     case 8: case 9: case 10: case 11: return gemm2_launch(BF, EPI, id, g, s);
+    case 12: return launch_cfg<BF, EPI, 64, 64, 4, 1, 3>(g, s);
     default: return hipErrorInvalidValue;
   }
 }
 
-constexpr int NCFG = 12;
+constexpr int NCFG = 13;
+static_assert(GEMM_CFG_SKINNY == 12, "config 12 is the 64 x 64 tile");
 static_assert(GEMM_CFG_SPLITK == 2, "config 2 is the 128 x 64 tile");
 
 // Tile choice: a cost model per kernel family, time(cfg) ~ rounds(cfg) x round_cost(cfg),
@@ -382,7 +384,7 @@ hipError_t gemm_cfg(bool bf16, int epi, int config, const GemmArgs& g, hipStream
   int id = config >= 0 ? config : pick_config(epi, g.M, g.N);
   if (g.K % BK) {   // the half last K-step: gemm_kernel configs without split-K only
     if (g.ksplit > 1) return hipErrorInvalidValue;
-    if (id >= 8) {
+    if (id >= 8 && id <= 11) {
       if (config >= 0) return hipErrorInvalidValue;
       id = pick_from(MODELS, g.M, g.N);
     }

@@ -55,6 +55,9 @@ inline size_t gemm_splitk_ws_bytes(int M, int N, int slices) { return (size_t)sl
 // explicit tile configuration (config < 0: heuristic); configs: k_gemm.hip launch_id.
 // GEMM_CFG_SPLITK: the 128 x 64 tile (4 waves), for few-row GEMMs (the pooled last layer)
 constexpr int GEMM_CFG_SPLITK = 2;
+// GEMM_CFG_SKINNY: 64 x 64 tiles (4 waves), for N <= 64 (the unmerged-LoRA down-projections): twice
+// the workgroups of 128 x 64 over the same rows
+constexpr int GEMM_CFG_SKINNY = 12;
 hipError_t gemm_cfg(bool bf16, int epi, int config, const GemmArgs& g, hipStream_t s);
 int gemm_num_configs();
 // host-side hint for the tile heuristic of the calling thread: true while two towers are being
