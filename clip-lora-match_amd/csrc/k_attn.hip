@@ -437,6 +437,193 @@ __global__ __launch_bounds__(256, SUB32 ? 4 : 2) void attn_long_kernel(const u16
                                               pack2<BF>(o[db][4 * g + 2] * inv, o[db][4 * g + 3] * inv)};
 }
 
+// V^T operand as v_frag32, from a V tile whose 16-B chunks are XOR-swizzled by
+// ((key >> 1) & 1) << 2 instead of K's (key >> 1) & 7: a ds_read_b64_tr_b16 bank group (32 lanes)
+// covers 4 consecutive key rows x 4 chunks, and this swizzle puts rows k and k + 2 in opposite
+// 64-B halves of the 128-B row, so the 32 lanes hit 32 distinct 8-B bank slots (K's swizzle maps
+// rows k and k + 2 onto the same four chunks: a 2-way conflict on every V read).
+__device__ __forceinline__ int swz_v(int row, int chunk) { return chunk ^ (((row >> 1) & 1) << 2); }
+__device__ __forceinline__ u32x4 v_frag32v(const uint8_t* tile, int k16, int dim0, int lane) {
+  const int gg = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
+  const int hi = gg >> 1, dh = gg & 1;
+  const int chunk = (dim0 >> 3) + 2 * dh + (p >> 1);
+  const int ka = k16 + 4 * hi + q, kb = ka + 8;
+  const uint8_t* pa = tile + ka * 128 + (swz_v(ka, chunk) << 4) + (p & 1) * 8;
+  const uint8_t* pb = tile + kb * 128 + (swz_v(kb, chunk) << 4) + (p & 1) * 8;
+  // inline asm, not the builtin: with global_load_lds DMAs in flight the compiler puts an
+  // s_waitcnt vmcnt(0) before every builtin transposed read (it cannot tell the DMA's buffer from
+  // this one), which would stall each tile on the next tile's DMA. The caller waits on lgkmcnt
+  // (lds_wait) before using the fragment.
+  const uint32_t la = (uint32_t)(uintptr_t)((__attribute__((address_space(3))) const uint8_t*)pa);
+  const uint32_t lb = (uint32_t)(uintptr_t)((__attribute__((address_space(3))) const uint8_t*)pb);
+  u32x2 a, b;
+  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(a) : "v"(la));
+  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(b) : "v"(lb));
+  return u32x4{a.x, a.y, b.x, b.y};
+}
+// every LDS read issued so far has landed; the fragments are tied to the wait so that no use of
+// them is scheduled above it
+__device__ __forceinline__ void lds_wait(u32x4& a, u32x4& b) {
+  asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(a), "+v"(b));
+}
+
+// T > 128, non-causal (ViT-L/14@336: T = 577), the default form. Same work split and MFMA shapes
+// as attn_long_kernel<BF, true> (4 waves x 32 queries of one (batch, head); 32-key online-softmax
+// steps on 32x32x16 MFMAs, S^T = K Q^T so a lane owns one query), rebuilt around its measured
+// bound -- vector-instruction issue (profiles/r05_v4_attn_pmc_summary.json: 2,459 VALU
+// instructions per wave, VALU active 21 % of every one of 4 waves per SIMD, MFMA busy 31 %):
+//   * K / V tiles stream HBM/L2 -> LDS by global_load_lds_dwordx4 (no register staging, no
+//     ds_write, no zero fill): each wave issues 2 K + 2 V pieces of 8 rows x 128 B per 64-key tile,
+//     rows past T clamped to T - 1 (their scores are masked to -inf, so P = 0 multiplies finite
+//     V rows); double-buffered, the DMA of tile kt + 1 issued right after the barrier that opens
+//     tile kt (every wave is then done with its buffer): one barrier per tile;
+//   * lazy max: P = exp2(S log2e - m) against the running max m as it stands, and the lane's sum of
+//     its 16 probabilities checked instead of a max over the scores. Only when some lane's sum
+//     exceeds 2^15 (a score more than ~11 log2-units above m, or m still -inf on the first step:
+//     the sum is then inf / NaN) does the wave take the exact rescale path (max over scores,
+//     v_permlane32_swap, O and the sum scaled by exp2(m - m_new), P recomputed). The fast path thus
+//     drops the 11-instruction max chain, the cross-lane swap and the vote on m per 32 keys; every
+//     P stays <= 2^15 (fp16-safe) and O / l is unchanged in exact arithmetic (a common factor);
+//   * V swizzled by swz_v (conflict-free transposed reads; K keeps swz for its ds_read_b128).
+template <bool BF>
+__global__ __launch_bounds__(256, 4) void attn_long_dma_kernel(const u16* qkv, int64_t ldq, u16* out, int64_t ldo,
+                                                               int T, int d, int H, int nqb) {
+  constexpr float L2E = 1.4426950408889634f;
+  constexpr float RS_MAX = 32768.f;
+  __shared__ __attribute__((aligned(16))) uint8_t smem[2 * 16384];
+  const int nwg = gridDim.x;
+  const int wg = xcd_remap(blockIdx.x, nwg);
+  const int qb = wg % nqb, bh = wg / nqb, h = bh % H, b = bh / H;
+  const int tid = threadIdx.x, lane = tid & 63, hi = lane >> 5;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const u16* base = qkv + (int64_t)b * T * ldq + h * 64;
+  const int qw = qb * 128 + wid * 32;   // first query of this wave
+  const bool active = qw < T;
+  const int qi = qw + (lane & 31);
+
+  // this lane's DMA slots: piece j of the wave covers tile rows (2 wid + j) * 8 .. + 7; lane ->
+  // row + (lane >> 3), LDS chunk position lane & 7, which holds the global chunk swz^-1 of it
+  const int r8 = lane >> 3, pc = lane & 7;
+  int kc[2], vc[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int row = (2 * wid + j) * 8 + r8;
+    kc[j] = d + swz(row, pc) * 8;
+    vc[j] = 2 * d + swz_v(row, pc) * 8;
+  }
+  auto issue = [&](int kt, int buf) {
+    uint8_t* sK = smem + buf * 16384;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int kg = min(kt * 64 + (2 * wid + j) * 8 + r8, T - 1);
+      const u16* rp = base + (int64_t)kg * ldq;
+      __builtin_amdgcn_global_load_lds((const void*)(rp + kc[j]), (void*)(sK + (2 * wid + j) * 1024), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((const void*)(rp + vc[j]), (void*)(sK + 8192 + (2 * wid + j) * 1024), 16, 0,
+                                       0);
+    }
+  };
+
+  u32x4 qf[4];   // Q^T operand: query qi, dims 16 s + 8 hi + 0..7
+  {
+    const u16* qp = base + (int64_t)min(qi, T - 1) * ldq + 8 * hi;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) qf[s] = *(const u32x4*)(qp + 16 * s);
+  }
+  f32x16 o[2];   // O^T: query qi, dims db * 32 + 8 (r >> 2) + 4 hi + (r & 3)
+#pragma unroll
+  for (int db = 0; db < 2; ++db)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) o[db][r] = 0.f;
+  float m = -INFINITY, l = 0.f;   // running shift (log2 domain, equal in lanes l, l ^ 32); lane-partial sum
+
+  const int nkt = (T + 63) / 64;
+  issue(0, 0);
+  for (int kt = 0; kt < nkt; ++kt) {
+    // this wave's pieces of tile kt landed; then every wave's, and every wave is done with tile
+    // kt - 1's buffer
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    if (kt + 1 < nkt) issue(kt + 1, (kt + 1) & 1);
+    if (!active) continue;
+    const uint8_t* sK = smem + (kt & 1) * 16384;
+    const uint8_t* sV = sK + 8192;
+    const int kleft = T - kt * 64;   // valid keys in this tile (>= 1)
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb) {
+      if (kb * 32 >= kleft) break;   // wave-uniform
+      f32x16 sc;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) sc[r] = 0.f;
+      const int krow = kb * 32 + (lane & 31);
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        const u32x4 kf = *(const u32x4*)(sK + krow * 128 + swz(krow, 2 * s + hi) * 16);
+        sc = mfma32<BF>(kf, qf[s], sc);
+      }
+      if (kleft < kb * 32 + 32) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          if (kb * 32 + 8 * (r >> 2) + 4 * hi + (r & 3) >= kleft) sc[r] = -INFINITY;
+      }
+      u32x4 pf[2];
+      float rs = 0.f;
+#pragma unroll
+      for (int hf = 0; hf < 2; ++hf) {
+        float p[8];
+#pragma unroll
+        for (int t = 0; t < 8; ++t) {
+          p[t] = __builtin_amdgcn_exp2f(fmaf(sc[8 * hf + t], L2E, -m));
+          rs += p[t];
+        }
+        pf[hf] = u32x4{pack2<BF>(p[0], p[1]), pack2<BF>(p[2], p[3]), pack2<BF>(p[4], p[5]), pack2<BF>(p[6], p[7])};
+      }
+      if (__any(!(rs <= RS_MAX))) {   // rare: rescale to the exact running max, recompute P
+        float tmax = sc[0];
+#pragma unroll
+        for (int r = 1; r < 16; ++r) tmax = fmaxf(tmax, sc[r]);
+        tmax = pair32_max(tmax);
+        const float mnew = fmaxf(m, tmax * L2E);   // finite: every processed half holds a valid key
+        const float alpha = __builtin_amdgcn_exp2f(m - mnew);
+        l *= alpha;
+#pragma unroll
+        for (int db = 0; db < 2; ++db)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) o[db][r] *= alpha;
+        m = mnew;
+        rs = 0.f;
+#pragma unroll
+        for (int hf = 0; hf < 2; ++hf) {
+          float p[8];
+#pragma unroll
+          for (int t = 0; t < 8; ++t) {
+            p[t] = __builtin_amdgcn_exp2f(fmaf(sc[8 * hf + t], L2E, -m));
+            rs += p[t];
+          }
+          pf[hf] = u32x4{pack2<BF>(p[0], p[1]), pack2<BF>(p[2], p[3]), pack2<BF>(p[4], p[5]), pack2<BF>(p[6], p[7])};
+        }
+      }
+      l += rs;
+#pragma unroll
+      for (int hf = 0; hf < 2; ++hf) {
+        u32x4 v0 = v_frag32v(sV, kb * 32 + 16 * hf, 0, lane), v1 = v_frag32v(sV, kb * 32 + 16 * hf, 32, lane);
+        lds_wait(v0, v1);
+        o[0] = mfma32<BF>(v0, pf[hf], o[0]);
+        o[1] = mfma32<BF>(v1, pf[hf], o[1]);
+      }
+    }
+  }
+  if (!active) return;
+  l = pair32_sum(l);
+  if (qi >= T) return;
+  const float inv = 1.0f / l;
+  u16* op = out + ((int64_t)b * T + qi) * ldo + h * 64 + 4 * hi;
+#pragma unroll
+  for (int db = 0; db < 2; ++db)
+#pragma unroll
+    for (int g = 0; g < 4; ++g)
+      *(u32x2*)(op + db * 32 + 8 * g) = u32x2{pack2<BF>(o[db][4 * g] * inv, o[db][4 * g + 1] * inv),
+                                              pack2<BF>(o[db][4 * g + 2] * inv, o[db][4 * g + 3] * inv)};
+}
+
 // T <= 128 (ViT-B/32: vision T = 50, text T = 77 causal): one workgroup per (head, batch),
 // ceil(T/16) waves x 16 queries; all key tiles (<= 2 x 64) of K and V staged once. Scores are
 // transposed as in attn_kernel (lane = one query, 16 keys per tile), and since every key is
@@ -560,13 +747,17 @@ hipError_t attention(bool bf16, bool causal, const u16* qkv, int64_t ldq, u16* o
     return hipGetLastError();
   }
   // $CLM_ATTN_LONG: 0 = the 16x16x32 attn_kernel, 1 = attn_long_kernel with 64-key softmax
-  // steps, 2 (default) = its SUB32 form (L/14: 6.53 vs 6.91 ms per step, profiles/r02_v4_attn_ab.txt)
-  static const int long_mode = getenv("CLM_ATTN_LONG") ? atoi(getenv("CLM_ATTN_LONG")) : 2;
+  // steps, 2 = its SUB32 form (L/14: 6.53 vs 6.91 ms per step, profiles/r02_v4_attn_ab.txt),
+  // 3 (default) = attn_long_dma_kernel
+  static const int long_mode = getenv("CLM_ATTN_LONG") ? atoi(getenv("CLM_ATTN_LONG")) : 3;
   if (!causal && long_mode) {
     const int nqb = (T + 127) / 128;
     const int64_t nwg = (int64_t)nqb * H * B;
     if (nwg > 0x7FFFFFFF) return hipErrorInvalidValue;
-    if (long_mode == 2) {
+    if (long_mode == 3) {
+      if (bf16) attn_long_dma_kernel<true><<<(unsigned)nwg, 256, 0, s>>>(qkv, ldq, out, ldo, T, d, H, nqb);
+      else attn_long_dma_kernel<false><<<(unsigned)nwg, 256, 0, s>>>(qkv, ldq, out, ldo, T, d, H, nqb);
+    } else if (long_mode == 2) {
       if (bf16) attn_long_kernel<true, true><<<(unsigned)nwg, 256, 0, s>>>(qkv, ldq, out, ldo, T, d, H, nqb);
       else attn_long_kernel<false, true><<<(unsigned)nwg, 256, 0, s>>>(qkv, ldq, out, ldo, T, d, H, nqb);
     } else {

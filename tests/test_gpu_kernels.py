@@ -143,18 +143,19 @@ def _attn_ref(qkv, B, T, H, causal):
                                                (1, 577, 16, False, 0), (2, 130, 2, True, 0), (1, 1, 2, True, 0),
                                                (2, 130, 2, False, 0), (2, 160, 3, False, 0), (1, 193, 2, False, 0),
                                                (2, 250, 4, False, 0), (1, 577, 2, False, 1), (1, 577, 2, False, -1),
-                                               (1, 700, 3, False, 1)])
+                                               (1, 700, 3, False, 1), (1, 577, 2, False, 2), (2, 300, 2, False, 2)])
 def test_attention_vs_torch(dtype, B, T, H, causal, ramp):
     """T > 128 non-causal runs the 32x32x16 online-softmax kernel: tail tiles of 2 / 32 / 1 / 58
     keys, and key magnitudes ramped up (the running max grows tile after tile: every rescale
-    fires) or down (none after the first tile)."""
+    fires), steeply up (ramp 2: the scores outgrow the lazy shift by far more than 2^15, so the
+    exact-rescale path runs on later tiles too) or down (none after the first tile)."""
     td = DT[dtype][0]
     g = torch.Generator(device="cuda").manual_seed(T * H)
     qkv = torch.randn((B * T, 3 * H * 64), generator=g, device="cuda")
     qkv[:, : H * 64] *= 0.125 * 3
     if ramp:
         t = torch.linspace(0.0, 1.0, T, device="cuda").repeat(B)
-        f = 0.5 + 2.0 * (t if ramp > 0 else 1.0 - t)
+        f = 0.5 + (2.0 if abs(ramp) == 1 else 12.0) * (t if ramp > 0 else 1.0 - t)
         qkv[:, H * 64: 2 * H * 64] *= f[:, None]
     qkv = qkv.to(td)
     out = torch.full((B * T, H * 64 + 64), 7.0, device="cuda").to(td)
