@@ -16,6 +16,7 @@ LIB_PATH = os.environ.get("CLM_LIB", os.path.join(_HERE, "libclm.so"))
 
 CLM_OK, CLM_E_ARG, CLM_E_OOM, CLM_E_HIP, CLM_E_STATE, CLM_E_MISSING = 0, -1, -2, -3, -4, -5
 CLM_F32, CLM_F16, CLM_BF16, CLM_U8, CLM_I32, CLM_I64 = 0, 1, 2, 3, 4, 5
+CLM_ATTN_CAUSAL, CLM_ATTN_Q_LOG2E = 1, 2   # clm_attention flags
 CLM_PIX_U8_HWC, CLM_PIX_F32_CHW = 0, 1
 CLM_LORA_MERGED, CLM_LORA_UNMERGED = 0, 1
 CLM_COMPUTE_MIXED = 0x12   # bf16 vision tower, fp16 text tower (clm.h)

@@ -117,6 +117,7 @@ struct LayerW {
 
 struct Tower {
   bool vision = false;
+  bool q_log2e = false;   // q_proj weights carry log2(e) (attention_folds_log2e)
   int d = 0, L = 0, H = 0, mlp = 0;
   std::vector<LayerW> layers;
   float *projT = nullptr, *fin_g = nullptr, *fin_b = nullptr;
@@ -299,7 +300,7 @@ struct LinearSpec {
 // Build a fused [sum(out), K] weight (fp32 host) for linears sharing one input.
 // merged: W += s * B A.  unmerged: K = in + RPAD, columns [in + off, in + off + r) = s * B.
 // Also returns the stacked A [r_ext, in] for the unmerged mode.
-int build_fused(clm_ctx* c, const std::vector<LinearSpec>& specs, bool q_scale_first, std::vector<float>& W,
+int build_fused(clm_ctx* c, const std::vector<LinearSpec>& specs, float q_scale, std::vector<float>& W,
                 std::vector<float>& bias, int& K, std::vector<float>& A_stack, int& r_ext, int& K_log) {
   const clm_model_desc& d = c->desc;
   const bool unmerged = d.lora_mode == CLM_LORA_UNMERGED;
@@ -325,7 +326,7 @@ int build_fused(clm_ctx* c, const std::vector<LinearSpec>& specs, bool q_scale_f
     if (r) return r;
     r = need(c, s.path + ".bias", s.out, &b);
     if (r) return r;
-    const float qs = (q_scale_first && si == 0) ? 0.125f : 1.0f;  // head_dim 64 -> 64^-1/2
+    const float qs = si == 0 ? q_scale : 1.0f;   // the first linear's scale (q_proj: see build_tower)
     for (int o = 0; o < s.out; ++o) {
       std::memcpy(&W[(size_t)(row0 + o) * K], &w->data[(size_t)o * s.in], s.in * sizeof(float));
       bias[row0 + o] = b->data[o];
@@ -378,6 +379,12 @@ int build_tower(clm_ctx* c, Tower& T, bool vision) {
   const bool lora_on = c->lora_enabled && d.lora_r > 0;
   const uint32_t tg = lora_on ? d.lora_targets : 0u;
   const bool unmerged = d.lora_mode == CLM_LORA_UNMERGED;
+  // q_proj carries the 64^-1/2 score scale (head_dim 64: a power of two, bit-identical to scaling
+  // the scores), and log2(e) too where the tower's attention kernel takes its scores in the log2
+  // domain (attention_folds_log2e: the L/14 image tower's T = 577)
+  const int Tseq = vision ? (d.image_size / d.patch) * (d.image_size / d.patch) + 1 : 0;
+  T.q_log2e = vision && attention_folds_log2e(c->bf16(true), false, Tseq);
+  const float qscale = T.q_log2e ? 0.125f * 1.4426950408889634f : 0.125f;
   int r;
   T.layers.resize(T.L);
   for (int l = 0; l < T.L; ++l) {
@@ -393,25 +400,25 @@ int build_tower(clm_ctx* c, Tower& T, bool vision) {
     std::vector<LinearSpec> qkv = {{p + ".self_attn.q_proj", T.d, T.d, (tg & CLM_LORA_Q) != 0},
                                    {p + ".self_attn.k_proj", T.d, T.d, (tg & CLM_LORA_K) != 0},
                                    {p + ".self_attn.v_proj", T.d, T.d, (tg & CLM_LORA_V) != 0}};
-    if ((r = build_fused(c, qkv, true, W, b, K, A, rext, KL))) return r;
+    if ((r = build_fused(c, qkv, qscale, W, b, K, A, rext, KL))) return r;
     if ((r = upload_16(c, W, &Lw.w_qkv, c->bf16(vision))) || (r = upload_f32(c, b, &Lw.b_qkv))) return r;
     Lw.k_qkv = K; Lw.kl_qkv = KL; Lw.r_qkv = rext;
     if (unmerged && rext && (r = upload_lora_a(c, A, rext, T.d, &Lw.a_qkv, c->bf16(vision)))) return r;
 
     std::vector<LinearSpec> outp = {{p + ".self_attn.out_proj", T.d, T.d, (tg & CLM_LORA_OUT) != 0}};
-    if ((r = build_fused(c, outp, false, W, b, K, A, rext, KL))) return r;
+    if ((r = build_fused(c, outp, 1.0f, W, b, K, A, rext, KL))) return r;
     if ((r = upload_16(c, W, &Lw.w_out, c->bf16(vision))) || (r = upload_f32(c, b, &Lw.b_out))) return r;
     Lw.k_out = K; Lw.kl_out = KL; Lw.r_out = rext;
     if (unmerged && rext && (r = upload_lora_a(c, A, rext, T.d, &Lw.a_out, c->bf16(vision)))) return r;
 
     std::vector<LinearSpec> fc1 = {{p + ".mlp.fc1", T.d, T.mlp, (tg & CLM_LORA_FC1) != 0}};
-    if ((r = build_fused(c, fc1, false, W, b, K, A, rext, KL))) return r;
+    if ((r = build_fused(c, fc1, 1.0f, W, b, K, A, rext, KL))) return r;
     if ((r = upload_16(c, W, &Lw.w_fc1, c->bf16(vision))) || (r = upload_f32(c, b, &Lw.b_fc1))) return r;
     Lw.k_fc1 = K; Lw.kl_fc1 = KL; Lw.r_fc1 = rext;
     if (unmerged && rext && (r = upload_lora_a(c, A, rext, T.d, &Lw.a_fc1, c->bf16(vision)))) return r;
 
     std::vector<LinearSpec> fc2 = {{p + ".mlp.fc2", T.mlp, T.d, (tg & CLM_LORA_FC2) != 0}};
-    if ((r = build_fused(c, fc2, false, W, b, K, A, rext, KL))) return r;
+    if ((r = build_fused(c, fc2, 1.0f, W, b, K, A, rext, KL))) return r;
     if ((r = upload_16(c, W, &Lw.w_fc2, c->bf16(vision))) || (r = upload_f32(c, b, &Lw.b_fc2))) return r;
     Lw.k_fc2 = K; Lw.kl_fc2 = KL; Lw.r_fc2 = rext;
     if (unmerged && rext && (r = upload_lora_a(c, A, rext, T.mlp, &Lw.a_fc2, c->bf16(vision)))) return r;
@@ -649,7 +656,7 @@ int attn_step(clm_ctx* c, const LayerRun& R, int l, hipStream_t st) {
   } else {
     { PROF(CLM_PROF_GEMM, 2.0 * g.M * g.N * g.K); KCHK(gemm(bf, EPI_STORE, g, st)); }
     { PROF(CLM_PROF_ATTN, 4.0 * R.B * T.H * (double)R.S * R.S * 64);
-      KCHK(attention(bf, R.causal, T.QKV, 3 * T.d, T.O, T.ldo, R.B, R.S, T.H, T.d, st)); }
+      KCHK(attention(bf, R.causal, T.QKV, 3 * T.d, T.O, T.ldo, R.B, R.S, T.H, T.d, st, T.q_log2e)); }
   }
   return CLM_OK;
 }
@@ -990,8 +997,12 @@ int clm_attention(int hip_device, int dtype, int causal, const void* qkv, void* 
   if (dtype != CLM_BF16 && dtype != CLM_F16) return fail(CLM_E_ARG, "dtype must be bf16 or f16");
   if (B < 0 || T < 0 || H <= 0) return fail(CLM_E_ARG, "bad shape");
   DeviceGuard g(hip_device);
-  hipError_t e = attention(dtype == CLM_BF16, causal != 0, (const u16*)qkv, 3LL * H * 64, (u16*)out, ldo, B, T, H,
-                           H * 64, (hipStream_t)stream);
+  if (causal & ~(CLM_ATTN_CAUSAL | CLM_ATTN_Q_LOG2E)) return fail(CLM_E_ARG, "unknown attention flags");
+  const bool bf = dtype == CLM_BF16, cz = (causal & CLM_ATTN_CAUSAL) != 0, l2e = (causal & CLM_ATTN_Q_LOG2E) != 0;
+  if (l2e && !attention_folds_log2e(bf, cz, T))
+    return fail(CLM_E_ARG, "CLM_ATTN_Q_LOG2E: the kernel for this dtype / mask / T takes q without log2(e)");
+  hipError_t e = attention(bf, cz, (const u16*)qkv, 3LL * H * 64, (u16*)out, ldo, B, T, H, H * 64,
+                           (hipStream_t)stream, l2e);
   if (e != hipSuccess) return fail(CLM_E_HIP, std::string("attention: ") + hipGetErrorString(e));
   return CLM_OK;
 }

@@ -19,6 +19,7 @@ namespace clm {
 namespace {
 
 typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) void* lds_ptr_t;
 
 // V^T operand of O^T = V^T P^T, from a ROW-MAJOR V tile ([64 keys][128 B], 16-B chunks
 // XOR-swizzled by (key>>1)&7 like K) with two ds_read_b64_tr_b16 (per 16-lane group, lane
@@ -443,22 +444,28 @@ __global__ __launch_bounds__(256, SUB32 ? 4 : 2) void attn_long_kernel(const u16
 // 64-B halves of the 128-B row, so the 32 lanes hit 32 distinct 8-B bank slots (K's swizzle maps
 // rows k and k + 2 onto the same four chunks: a 2-way conflict on every V read).
 __device__ __forceinline__ int swz_v(int row, int chunk) { return chunk ^ (((row >> 1) & 1) << 2); }
-__device__ __forceinline__ u32x4 v_frag32v(const uint8_t* tile, int k16, int dim0, int lane) {
+
+// this lane's V^T read address (LDS bytes, tile at tile0) for dims db * 32 .., key rows 4 hi + q:
+// lane l (hi = l >> 5) reads dim db * 32 + (l & 31)'s keys in the order the S^T accumulator holds P.
+// The swizzle term depends only on (q >> 1) & 1, so each key block k16 (and its +8 partner) is an
+// immediate offset on this one address.
+__device__ __forceinline__ uint32_t v_lane_base(uint32_t tile0, int db, int lane) {
   const int gg = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
   const int hi = gg >> 1, dh = gg & 1;
-  const int chunk = (dim0 >> 3) + 2 * dh + (p >> 1);
-  const int ka = k16 + 4 * hi + q, kb = ka + 8;
-  const uint8_t* pa = tile + ka * 128 + (swz_v(ka, chunk) << 4) + (p & 1) * 8;
-  const uint8_t* pb = tile + kb * 128 + (swz_v(kb, chunk) << 4) + (p & 1) * 8;
-  // inline asm, not the builtin: with global_load_lds DMAs in flight the compiler puts an
-  // s_waitcnt vmcnt(0) before every builtin transposed read (it cannot tell the DMA's buffer from
-  // this one), which would stall each tile on the next tile's DMA. The caller waits on lgkmcnt
-  // (lds_wait) before using the fragment.
-  const uint32_t la = (uint32_t)(uintptr_t)((__attribute__((address_space(3))) const uint8_t*)pa);
-  const uint32_t lb = (uint32_t)(uintptr_t)((__attribute__((address_space(3))) const uint8_t*)pb);
+  const int chunk = db * 4 + 2 * dh + (p >> 1);
+  const int ka = 4 * hi + q;
+  return tile0 + ka * 128 + (swz_v(ka, chunk) << 4) + (p & 1) * 8;
+}
+// V^T fragment (32 dims x 16 keys) at byte offset OFF from the lane's base: two
+// ds_read_b64_tr_b16 (rows k16 + 4 hi + q and + 8). Inline asm, not the builtin: with LDS DMAs in
+// flight the compiler puts an s_waitcnt vmcnt(0) before every builtin transposed read (it cannot
+// tell the DMA's buffer from this one), which would stall each tile on the next tile's DMA; the
+// caller waits on lgkmcnt (lds_wait) before using the fragment.
+template <int OFF>
+__device__ __forceinline__ u32x4 v_frag32v(uint32_t va) {
   u32x2 a, b;
-  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(a) : "v"(la));
-  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(b) : "v"(lb));
+  asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(a) : "v"(va), "i"(OFF));
+  asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(b) : "v"(va), "i"(OFF + 8 * 128));
   return u32x4{a.x, a.y, b.x, b.y};
 }
 // every LDS read issued so far has landed; the fragments are tied to the wait so that no use of
@@ -466,17 +473,20 @@ __device__ __forceinline__ u32x4 v_frag32v(const uint8_t* tile, int k16, int dim
 __device__ __forceinline__ void lds_wait(u32x4& a, u32x4& b) {
   asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(a), "+v"(b));
 }
+template <int N> struct IC { static constexpr int value = N; };
 
 // T > 128, non-causal (ViT-L/14@336: T = 577), the default form. Same work split and MFMA shapes
 // as attn_long_kernel<BF, true> (4 waves x 32 queries of one (batch, head); 32-key online-softmax
 // steps on 32x32x16 MFMAs, S^T = K Q^T so a lane owns one query), rebuilt around its measured
 // bound -- vector-instruction issue (profiles/r05_v4_attn_pmc_summary.json: 2,459 VALU
 // instructions per wave, VALU active 21 % of every one of 4 waves per SIMD, MFMA busy 31 %):
-//   * K / V tiles stream HBM/L2 -> LDS by global_load_lds_dwordx4 (no register staging, no
-//     ds_write, no zero fill): each wave issues 2 K + 2 V pieces of 8 rows x 128 B per 64-key tile,
-//     rows past T clamped to T - 1 (their scores are masked to -inf, so P = 0 multiplies finite
-//     V rows); double-buffered, the DMA of tile kt + 1 issued right after the barrier that opens
-//     tile kt (every wave is then done with its buffer): one barrier per tile;
+//   * K / V tiles stream HBM/L2 -> LDS by buffer_load ... lds (no register staging, no ds_write,
+//     no zero fill, no per-tile address arithmetic): each wave issues 2 K + 2 V pieces of 8 rows x
+//     128 B per 64-key tile from a per-tile buffer resource over the rows left, so rows past T
+//     read as zeros (their scores are masked to -inf anyway); double-buffered, the DMA of tile
+//     kt + 1 issued right after the barrier that opens tile kt (every wave is then done with its
+//     buffer): one barrier per tile. The tile loop is unrolled by two so both buffers' LDS
+//     offsets are immediates of the fragment reads;
 //   * lazy max: P = exp2(S log2e - m) against the running max m as it stands, and the lane's sum of
 //     its 16 probabilities checked instead of a max over the scores. Only when some lane's sum
 //     exceeds 2^15 (a score more than ~11 log2-units above m, or m still -inf on the first step:
@@ -485,10 +495,17 @@ __device__ __forceinline__ void lds_wait(u32x4& a, u32x4& b) {
 //     drops the 11-instruction max chain, the cross-lane swap and the vote on m per 32 keys; every
 //     P stays <= 2^15 (fp16-safe) and O / l is unchanged in exact arithmetic (a common factor);
 //   * V swizzled by swz_v (conflict-free transposed reads; K keeps swz for its ds_read_b128).
-template <bool BF>
+// QL2E (bf16 only): q arrives pre-scaled by log2(e) as well (the engine folds it into the q_proj
+// weights, attention_folds_log2e), so the scores are already in the log2 domain, and the running
+// shift m -- kept as a bf16 value -- enters the score accumulator through a fifth MFMA of the QK
+// chain (A = a column of ones, B = -m in k-slot 0): the fast path is then P = exp2(acc), without
+// the 16 v_fma_f32 per 32 keys that apply log2 e and subtract m (one 32-cycle MFMA instead of 64
+// cycles of vector issue).
+template <bool BF, bool QL2E>
 __global__ __launch_bounds__(256, 4) void attn_long_dma_kernel(const u16* qkv, int64_t ldq, u16* out, int64_t ldo,
                                                                int T, int d, int H, int nqb) {
-  constexpr float L2E = 1.4426950408889634f;
+  static_assert(BF || !QL2E, "the folded form keeps the shift in bf16");
+  constexpr float L2E = QL2E ? 1.0f : 1.4426950408889634f;
   constexpr float RS_MAX = 32768.f;
   __shared__ __attribute__((aligned(16))) uint8_t smem[2 * 16384];
   const int nwg = gridDim.x;
@@ -500,26 +517,29 @@ __global__ __launch_bounds__(256, 4) void attn_long_dma_kernel(const u16* qkv, i
   const int qw = qb * 128 + wid * 32;   // first query of this wave
   const bool active = qw < T;
   const int qi = qw + (lane & 31);
+  const uint32_t lds0 = (uint32_t)(uintptr_t)((__attribute__((address_space(3))) uint8_t*)smem);
 
-  // this lane's DMA slots: piece j of the wave covers tile rows (2 wid + j) * 8 .. + 7; lane ->
-  // row + (lane >> 3), LDS chunk position lane & 7, which holds the global chunk swz^-1 of it
+  // this lane's DMA byte offsets: piece j of the wave covers tile rows (2 wid + j) * 8 .. + 7;
+  // lane -> row + (lane >> 3), LDS chunk position lane & 7, which holds the global chunk that the
+  // swizzle maps there
   const int r8 = lane >> 3, pc = lane & 7;
-  int kc[2], vc[2];
+  const uint32_t ldq2 = (uint32_t)ldq * 2;
+  uint32_t ko[2], vo[2];
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
     const int row = (2 * wid + j) * 8 + r8;
-    kc[j] = d + swz(row, pc) * 8;
-    vc[j] = 2 * d + swz_v(row, pc) * 8;
+    ko[j] = row * ldq2 + (uint32_t)(d + swz(row, pc) * 8) * 2;
+    vo[j] = row * ldq2 + (uint32_t)(2 * d + swz_v(row, pc) * 8) * 2;
   }
-  auto issue = [&](int kt, int buf) {
-    uint8_t* sK = smem + buf * 16384;
+  auto issue = [&](int kt, auto bufc) {
+    constexpr int BUF = decltype(bufc)::value;
+    const auto rs = buf_rsrc(base + (int64_t)kt * 64 * ldq, (T - kt * 64) * (int)ldq2);
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
-      const int kg = min(kt * 64 + (2 * wid + j) * 8 + r8, T - 1);
-      const u16* rp = base + (int64_t)kg * ldq;
-      __builtin_amdgcn_global_load_lds((const void*)(rp + kc[j]), (void*)(sK + (2 * wid + j) * 1024), 16, 0, 0);
-      __builtin_amdgcn_global_load_lds((const void*)(rp + vc[j]), (void*)(sK + 8192 + (2 * wid + j) * 1024), 16, 0,
-                                       0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_ptr_t)(smem + BUF * 16384 + (2 * wid + j) * 1024), 16, ko[j], 0,
+                                               0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_ptr_t)(smem + BUF * 16384 + 8192 + (2 * wid + j) * 1024), 16,
+                                               vo[j], 0, 0, 0);
     }
   };
 
@@ -529,87 +549,123 @@ __global__ __launch_bounds__(256, 4) void attn_long_dma_kernel(const u16* qkv, i
 #pragma unroll
     for (int s = 0; s < 4; ++s) qf[s] = *(const u32x4*)(qp + 16 * s);
   }
+  // K fragment rows: key kb * 32 + (lane & 31), chunk 2 s + hi (the kb / buffer parts are immediates)
+  uint32_t kaddr[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) kaddr[s] = (lane & 31) * 128 + swz(lane & 31, 2 * s + hi) * 16;
+  const uint32_t va0 = v_lane_base(lds0, 0, lane), va1 = v_lane_base(lds0, 1, lane);
+
   f32x16 o[2];   // O^T: query qi, dims db * 32 + 8 (r >> 2) + 4 hi + (r & 3)
 #pragma unroll
   for (int db = 0; db < 2; ++db)
 #pragma unroll
     for (int r = 0; r < 16; ++r) o[db][r] = 0.f;
-  float m = -INFINITY, l = 0.f;   // running shift (log2 domain, equal in lanes l, l ^ 32); lane-partial sum
+  float m = QL2E ? 0.f : -INFINITY;   // running shift (log2 domain, equal in lanes l, l ^ 32)
+  float l = 0.f;                      // lane-partial sum
+  // QL2E: the shift's MFMA operands (k-slot 0 of lanes 0..31; every other slot zero)
+  const u32x4 ones = u32x4{hi ? 0u : 0x3F80u, 0u, 0u, 0u};
+  u32x4 negm = u32x4{0u, 0u, 0u, 0u};
 
-  const int nkt = (T + 63) / 64;
-  issue(0, 0);
-  for (int kt = 0; kt < nkt; ++kt) {
-    // this wave's pieces of tile kt landed; then every wave's, and every wave is done with tile
-    // kt - 1's buffer
-    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    if (kt + 1 < nkt) issue(kt + 1, (kt + 1) & 1);
-    if (!active) continue;
-    const uint8_t* sK = smem + (kt & 1) * 16384;
-    const uint8_t* sV = sK + 8192;
-    const int kleft = T - kt * 64;   // valid keys in this tile (>= 1)
+  // one 32-key online-softmax step: keys kt * 64 + KB * 32 .. of the tile in buffer BUF
+  auto half = [&](int kt, int kleft, auto bufc, auto kbc) {
+    constexpr int BUF = decltype(bufc)::value, KB = decltype(kbc)::value;
+    constexpr int KOFF = BUF * 16384 + KB * 4096, VOFF = BUF * 16384 + 8192 + KB * 32 * 128;
+    const bool first = kt == 0 && KB == 0;
+    f32x16 sc;
 #pragma unroll
-    for (int kb = 0; kb < 2; ++kb) {
-      if (kb * 32 >= kleft) break;   // wave-uniform
-      f32x16 sc;
+    for (int r = 0; r < 16; ++r) sc[r] = 0.f;
+    if constexpr (QL2E) sc = mfma32<BF>(ones, negm, sc);   // sc = -m
 #pragma unroll
-      for (int r = 0; r < 16; ++r) sc[r] = 0.f;
-      const int krow = kb * 32 + (lane & 31);
+    for (int s = 0; s < 4; ++s) {
+      const u32x4 kf = *(const u32x4*)(smem + KOFF + kaddr[s]);
+      sc = mfma32<BF>(kf, qf[s], sc);
+    }
+    if (kleft < KB * 32 + 32) {
 #pragma unroll
-      for (int s = 0; s < 4; ++s) {
-        const u32x4 kf = *(const u32x4*)(sK + krow * 128 + swz(krow, 2 * s + hi) * 16);
-        sc = mfma32<BF>(kf, qf[s], sc);
+      for (int r = 0; r < 16; ++r)
+        if (KB * 32 + 8 * (r >> 2) + 4 * hi + (r & 3) >= kleft) sc[r] = -INFINITY;
+    }
+    u32x4 pf[2];
+    float rs = 0.f;
+#pragma unroll
+    for (int hf = 0; hf < 2; ++hf) {
+      float p[8];
+#pragma unroll
+      for (int t = 0; t < 8; ++t) {
+        p[t] = __builtin_amdgcn_exp2f(QL2E ? sc[8 * hf + t] : fmaf(sc[8 * hf + t], L2E, -m));
+        rs += p[t];
       }
-      if (kleft < kb * 32 + 32) {
+      pf[hf] = u32x4{pack2<BF>(p[0], p[1]), pack2<BF>(p[2], p[3]), pack2<BF>(p[4], p[5]), pack2<BF>(p[6], p[7])};
+    }
+    // rare: rescale to the exact running max, recompute P. QL2E: the first step always rescales
+    // (m = 0 is no running max: its probabilities could all underflow)
+    if ((QL2E && first) || __any(!(rs <= RS_MAX))) {
+      float tmax = sc[0];
 #pragma unroll
-        for (int r = 0; r < 16; ++r)
-          if (kb * 32 + 8 * (r >> 2) + 4 * hi + (r & 3) >= kleft) sc[r] = -INFINITY;
+      for (int r = 1; r < 16; ++r) tmax = fmaxf(tmax, sc[r]);
+      tmax = pair32_max(tmax);   // finite: every processed step holds a valid key
+      float dm;                  // the shift's growth; sc is relative to the old shift (QL2E)
+      if constexpr (QL2E) {
+        // the new shift, rounded to bf16 (it re-enters the MFMA as a bf16 operand); the
+        // difference of two bf16 values is exact in fp32
+        const uint32_t mb = pack2<true>(m + (first ? tmax : fmaxf(tmax, 0.f)), 0.f) & 0xFFFFu;
+        const float mnew = __uint_as_float(mb << 16);
+        dm = mnew - m;
+        m = mnew;
+        negm = u32x4{hi ? 0u : (mb ^ 0x8000u), 0u, 0u, 0u};
+      } else {
+        const float mnew = fmaxf(m, tmax * L2E);
+        dm = mnew - m;   // +inf on the first step: alpha = 0 scales the zero O and sum
+        m = mnew;
       }
-      u32x4 pf[2];
-      float rs = 0.f;
+      const float alpha = __builtin_amdgcn_exp2f(-dm);
+      l *= alpha;
+#pragma unroll
+      for (int db = 0; db < 2; ++db)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) o[db][r] *= alpha;
+      rs = 0.f;
 #pragma unroll
       for (int hf = 0; hf < 2; ++hf) {
         float p[8];
 #pragma unroll
         for (int t = 0; t < 8; ++t) {
-          p[t] = __builtin_amdgcn_exp2f(fmaf(sc[8 * hf + t], L2E, -m));
+          p[t] = __builtin_amdgcn_exp2f(QL2E ? sc[8 * hf + t] - dm : fmaf(sc[8 * hf + t], L2E, -m));
           rs += p[t];
         }
         pf[hf] = u32x4{pack2<BF>(p[0], p[1]), pack2<BF>(p[2], p[3]), pack2<BF>(p[4], p[5]), pack2<BF>(p[6], p[7])};
       }
-      if (__any(!(rs <= RS_MAX))) {   // rare: rescale to the exact running max, recompute P
-        float tmax = sc[0];
-#pragma unroll
-        for (int r = 1; r < 16; ++r) tmax = fmaxf(tmax, sc[r]);
-        tmax = pair32_max(tmax);
-        const float mnew = fmaxf(m, tmax * L2E);   // finite: every processed half holds a valid key
-        const float alpha = __builtin_amdgcn_exp2f(m - mnew);
-        l *= alpha;
-#pragma unroll
-        for (int db = 0; db < 2; ++db)
-#pragma unroll
-          for (int r = 0; r < 16; ++r) o[db][r] *= alpha;
-        m = mnew;
-        rs = 0.f;
-#pragma unroll
-        for (int hf = 0; hf < 2; ++hf) {
-          float p[8];
-#pragma unroll
-          for (int t = 0; t < 8; ++t) {
-            p[t] = __builtin_amdgcn_exp2f(fmaf(sc[8 * hf + t], L2E, -m));
-            rs += p[t];
-          }
-          pf[hf] = u32x4{pack2<BF>(p[0], p[1]), pack2<BF>(p[2], p[3]), pack2<BF>(p[4], p[5]), pack2<BF>(p[6], p[7])};
-        }
-      }
-      l += rs;
-#pragma unroll
-      for (int hf = 0; hf < 2; ++hf) {
-        u32x4 v0 = v_frag32v(sV, kb * 32 + 16 * hf, 0, lane), v1 = v_frag32v(sV, kb * 32 + 16 * hf, 32, lane);
-        lds_wait(v0, v1);
-        o[0] = mfma32<BF>(v0, pf[hf], o[0]);
-        o[1] = mfma32<BF>(v1, pf[hf], o[1]);
-      }
     }
+    l += rs;
+    {
+      u32x4 v0 = v_frag32v<VOFF>(va0), v1 = v_frag32v<VOFF>(va1);
+      lds_wait(v0, v1);
+      o[0] = mfma32<BF>(v0, pf[0], o[0]);
+      o[1] = mfma32<BF>(v1, pf[0], o[1]);
+    }
+    {
+      u32x4 v0 = v_frag32v<VOFF + 16 * 128>(va0), v1 = v_frag32v<VOFF + 16 * 128>(va1);
+      lds_wait(v0, v1);
+      o[0] = mfma32<BF>(v0, pf[1], o[0]);
+      o[1] = mfma32<BF>(v1, pf[1], o[1]);
+    }
+  };
+  const int nkt = (T + 63) / 64;
+  auto tile = [&](int kt, auto bufc) {
+    constexpr int BUF = decltype(bufc)::value;
+    // this wave's pieces of tile kt landed; then every wave's, and every wave is done with tile
+    // kt - 1's buffer
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    if (kt + 1 < nkt) issue(kt + 1, IC<1 - BUF>{});
+    if (!active) return;
+    const int kleft = T - kt * 64;   // valid keys in this tile (>= 1)
+    half(kt, kleft, bufc, IC<0>{});
+    if (kleft > 32) half(kt, kleft, bufc, IC<1>{});
+  };
+  issue(0, IC<0>{});
+  for (int kt = 0; kt < nkt; kt += 2) {
+    tile(kt, IC<0>{});
+    if (kt + 1 < nkt) tile(kt + 1, IC<1>{});
   }
   if (!active) return;
   l = pair32_sum(l);
@@ -724,12 +780,24 @@ __global__ __launch_bounds__(512) void attn_small_kernel(const u16* qkv, int64_t
   for (int nb = 0; nb < 4; ++nb)
     *(u32x2*)(op + nb * 16) = u32x2{pack2<BF>(o[nb][0] * inv, o[nb][1] * inv), pack2<BF>(o[nb][2] * inv, o[nb][3] * inv)};
 }
+// $CLM_ATTN_LONG (T > 128, non-causal): 0 = the 16x16x32 attn_kernel, 1 = attn_long_kernel with
+// 64-key softmax steps, 2 = its SUB32 form (L/14: 6.53 vs 6.91 ms per step,
+// profiles/r02_v4_attn_ab.txt), 3 (default) = attn_long_dma_kernel
+int attn_long_mode() {
+  static const int m = getenv("CLM_ATTN_LONG") ? atoi(getenv("CLM_ATTN_LONG")) : 3;
+  return m;
+}
 }  // namespace
 
+bool attention_folds_log2e(bool bf16, bool causal, int T) {
+  return bf16 && !causal && T > 128 && attn_long_mode() == 3;
+}
+
 hipError_t attention(bool bf16, bool causal, const u16* qkv, int64_t ldq, u16* out, int64_t ldo, int B, int T,
-                     int H, int d, hipStream_t s) {
-  if (B <= 0 || T <= 0) return hipSuccess;
+                     int H, int d, hipStream_t s, bool q_log2e) {
   if (d != H * 64 || (ldq % 8) || (ldo % 8)) return hipErrorInvalidValue;
+  if (q_log2e && !attention_folds_log2e(bf16, causal, T)) return hipErrorInvalidValue;
+  if (B <= 0 || T <= 0) return hipSuccess;
   if (T <= 128) {
     dim3 g2(H, B), b2(64 * ((T + 15) / 16));
     // NT = 1 for T <= 64 measured no faster in the pipeline (0.46-0.48 ms of attention per step
@@ -746,17 +814,15 @@ hipError_t attention(bool bf16, bool causal, const u16* qkv, int64_t ldq, u16* o
 #undef CLM_SMALL
     return hipGetLastError();
   }
-  // $CLM_ATTN_LONG: 0 = the 16x16x32 attn_kernel, 1 = attn_long_kernel with 64-key softmax
-  // steps, 2 = its SUB32 form (L/14: 6.53 vs 6.91 ms per step, profiles/r02_v4_attn_ab.txt),
-  // 3 (default) = attn_long_dma_kernel
-  static const int long_mode = getenv("CLM_ATTN_LONG") ? atoi(getenv("CLM_ATTN_LONG")) : 3;
+  const int long_mode = attn_long_mode();
   if (!causal && long_mode) {
     const int nqb = (T + 127) / 128;
     const int64_t nwg = (int64_t)nqb * H * B;
     if (nwg > 0x7FFFFFFF) return hipErrorInvalidValue;
     if (long_mode == 3) {
-      if (bf16) attn_long_dma_kernel<true><<<(unsigned)nwg, 256, 0, s>>>(qkv, ldq, out, ldo, T, d, H, nqb);
-      else attn_long_dma_kernel<false><<<(unsigned)nwg, 256, 0, s>>>(qkv, ldq, out, ldo, T, d, H, nqb);
+      if (q_log2e) attn_long_dma_kernel<true, true><<<(unsigned)nwg, 256, 0, s>>>(qkv, ldq, out, ldo, T, d, H, nqb);
+      else if (bf16) attn_long_dma_kernel<true, false><<<(unsigned)nwg, 256, 0, s>>>(qkv, ldq, out, ldo, T, d, H, nqb);
+      else attn_long_dma_kernel<false, false><<<(unsigned)nwg, 256, 0, s>>>(qkv, ldq, out, ldo, T, d, H, nqb);
     } else if (long_mode == 2) {
       if (bf16) attn_long_kernel<true, true><<<(unsigned)nwg, 256, 0, s>>>(qkv, ldq, out, ldo, T, d, H, nqb);
       else attn_long_kernel<false, true><<<(unsigned)nwg, 256, 0, s>>>(qkv, ldq, out, ldo, T, d, H, nqb);

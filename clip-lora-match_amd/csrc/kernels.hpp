@@ -155,8 +155,13 @@ hipError_t text_plan(const int32_t* ids, int B, int L, int eos, int* lens, int* 
 
 // ----------------------------------------------------------- attention -----
 // qkv [B*T, 3d] (q pre-scaled by head_dim^-0.5), out [B*T, ldo] compute dtype.
+// q_log2e: q carries log2(e) as well (the scores arrive in the log2 domain); valid only where
+// attention_folds_log2e(bf16, causal, T) -- the kernel chosen for that shape takes that form
+// (k_attn.hip attn_long_dma_kernel<true, true>: bf16, non-causal, T > 128) -- else
+// hipErrorInvalidValue. The engine folds log2 e into the q_proj weights of such towers.
+bool attention_folds_log2e(bool bf16, bool causal, int T);
 hipError_t attention(bool bf16, bool causal, const u16* qkv, int64_t ldq, u16* out, int64_t ldo,
-                     int B, int T, int H, int d, hipStream_t s);
+                     int B, int T, int H, int d, hipStream_t s, bool q_log2e = false);
 // fused q/k/v projection + attention (k_gemm_attn.hip), T <= 128: out = attention(X . Wqkv^T +
 // bias) without materialising QKV; bit-identical to gemm(EPI_STORE) + attention()
 bool gemm_attn_supported(int T, int H, int d, int K);

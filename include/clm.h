@@ -237,7 +237,13 @@ void clm_debug_set(int flags);
  * general path, k <= 1024); both give the same bits. */
 int clm_topk_threshold(int hip_device, const float* scores, int64_t lds, int64_t nq, int64_t C, int k,
                        float margin, int method, float* th, void* stream);
-/* attention over qkv [B*T, 3*H*64] (q pre-scaled), out [B*T, ldo] (device pointers) */
+/* attention over qkv [B*T, 3*H*64] (q pre-scaled by 64^-1/2), out [B*T, ldo] (device
+ * pointers). flags: CLM_ATTN_CAUSAL (1, the text tower's mask; the argument was a 0/1 causal
+ * switch and keeps that meaning), CLM_ATTN_Q_LOG2E (2): q carries log2(e) as well -- the form the
+ * engine uses where the kernel takes log2-domain scores (bf16, non-causal, T > 128); CLM_E_ARG
+ * for any other shape. */
+#define CLM_ATTN_CAUSAL 1
+#define CLM_ATTN_Q_LOG2E 2
 int clm_attention(int hip_device, int dtype, int causal, const void* qkv, void* out, int64_t ldo,
                   int B, int T, int H, void* stream);
 /* LayerNorm of fp32 rows src [M, lds] over d columns (d a multiple of 128, <= 1024), eps, fp32

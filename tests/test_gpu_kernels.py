@@ -167,6 +167,45 @@ def test_attention_vs_torch(dtype, B, T, H, causal, ramp):
     assert (out[:, H * 64:].float() == 7.0).all()   # columns past d untouched
 
 
+@pytest.mark.parametrize("B,T,H,ramp", [(1, 577, 16, 0), (2, 130, 2, 0), (1, 193, 2, 1), (2, 300, 2, 2),
+                                         (1, 577, 2, -1), (1, 700, 3, 2)])
+def test_attention_q_log2e_vs_torch(B, T, H, ramp):
+    """CLM_ATTN_Q_LOG2E (the engine's form for the L/14 image tower): q carries log2(e) too, the
+    running shift enters the score MFMA chain as a bf16 operand. Inputs as in the unfolded test,
+    q scaled by log2 e in fp32 and rounded once to bf16; the fp32 reference takes that same
+    rounded q with log2 e divided back out (so both see one q), same bar; the first-step and
+    2^15-sum rescale paths are exercised by the ramps."""
+    g = torch.Generator(device="cuda").manual_seed(T * H + 1)
+    qkv = torch.randn((B * T, 3 * H * 64), generator=g, device="cuda")
+    qkv[:, : H * 64] *= 0.125 * 3
+    if ramp:
+        t = torch.linspace(0.0, 1.0, T, device="cuda").repeat(B)
+        f = 0.5 + (2.0 if abs(ramp) == 1 else 12.0) * (t if ramp > 0 else 1.0 - t)
+        qkv[:, H * 64: 2 * H * 64] *= f[:, None]
+    folded = qkv.clone()
+    folded[:, : H * 64] *= 1.4426950408889634
+    folded = folded.to(torch.bfloat16)
+    ref_in = folded.float()   # the reference sees the same rounded q (log2 e divided back out in fp32)
+    ref_in[:, : H * 64] /= 1.4426950408889634
+    out = torch.full((B * T, H * 64 + 64), 7.0, device="cuda").to(torch.bfloat16)
+    C.check(C.lib().clm_attention(0, C.CLM_BF16, C.CLM_ATTN_Q_LOG2E, C.ptr(folded), C.ptr(out), out.stride(0), B, T,
+                                  H, C.stream_of(qkv.device)), "clm_attention")
+    ref = _attn_ref(ref_in, B, T, H, False)
+    err = (out[:, : H * 64].float() - ref).abs().max().item()
+    assert err < 3e-2, err
+    assert (out[:, H * 64:].float() == 7.0).all()
+
+
+@pytest.mark.parametrize("dtype,flags,T", [("float16", 2, 577), ("bfloat16", 3, 577), ("bfloat16", 2, 128),
+                                           ("bfloat16", 4, 577)])
+def test_attention_q_log2e_refused(dtype, flags, T):
+    """the log2(e) form exists only for the bf16, non-causal, T > 128 kernel; unknown flags refused"""
+    qkv = torch.zeros((T, 3 * 64), dtype=DT[dtype][0], device="cuda")
+    out = torch.zeros((T, 64), dtype=DT[dtype][0], device="cuda")
+    rc = C.lib().clm_attention(0, DT[dtype][1], flags, C.ptr(qkv), C.ptr(out), 64, 1, T, 1, C.stream_of(qkv.device))
+    assert rc == C.CLM_E_ARG
+
+
 def _rounding_probe(n, seed):
     """fp32 values that stress the fp32 -> 16-bit RNE conversion: every binade from fp16
     subnormals to past the fp16 overflow threshold, exact half-way ties, zero (acc + bias turns a -0 bias into +0, so none here)."""

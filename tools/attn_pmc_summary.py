@@ -10,6 +10,7 @@ import csv
 import glob
 import json
 import os
+import re
 import sys
 
 N_CU, SIMD_PER_CU, N_XCD = 256, 4, 8
@@ -23,7 +24,7 @@ def main(src="gpurun_out/apmc", tag="r05", kern="attn_long_kernel"):
         for r in csv.DictReader(open(f)):
             if kern not in r["Kernel_Name"]:
                 continue
-            names.add(r["Kernel_Name"].split("(")[0])
+            names.add(re.sub(r"\(.*", "", r["Kernel_Name"].replace("(anonymous namespace)", "anon")))
             per[r.get("Dispatch_Id") or r.get("Correlation_Id")][r["Counter_Name"]] += float(r["Counter_Value"])
         for cv in per.values():
             for c, v in cv.items():
