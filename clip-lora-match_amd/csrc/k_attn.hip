@@ -566,26 +566,29 @@ __global__ __launch_bounds__(256, 4) void attn_long_dma_kernel(const u16* qkv, i
   const u32x4 ones = u32x4{hi ? 0u : 0x3F80u, 0u, 0u, 0u};
   u32x4 negm = u32x4{0u, 0u, 0u, 0u};
 
-  // one 32-key online-softmax step: keys kt * 64 + KB * 32 .. of the tile in buffer BUF
-  auto half = [&](int kt, int kleft, auto bufc, auto kbc) {
+  // S^T of keys KB * 32 .. of the tile in buffer BUF (QL2E: minus the shift as it stands)
+  auto qk = [&](auto bufc, auto kbc, f32x16& sc) {
     constexpr int BUF = decltype(bufc)::value, KB = decltype(kbc)::value;
-    constexpr int KOFF = BUF * 16384 + KB * 4096, VOFF = BUF * 16384 + 8192 + KB * 32 * 128;
-    const bool first = kt == 0 && KB == 0;
-    f32x16 sc;
+    constexpr int KOFF = BUF * 16384 + KB * 4096;
+    u32x4 kf[4];   // all four K fragments in flight before the first QK MFMA
+#pragma unroll
+    for (int s = 0; s < 4; ++s) kf[s] = *(const u32x4*)(smem + KOFF + kaddr[s]);
 #pragma unroll
     for (int r = 0; r < 16; ++r) sc[r] = 0.f;
     if constexpr (QL2E) sc = mfma32<BF>(ones, negm, sc);   // sc = -m
 #pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      const u32x4 kf = *(const u32x4*)(smem + KOFF + kaddr[s]);
-      sc = mfma32<BF>(kf, qf[s], sc);
-    }
-    if (kleft < KB * 32 + 32) {
+    for (int s = 0; s < 4; ++s) sc = mfma32<BF>(kf[s], qf[s], sc);
+  };
+  // keys past T (kleft valid keys in the tile): register r holds key KB*32 + 8(r>>2) + 4hi + (r&3)
+  auto mask = [&](f32x16& sc, int kleft, int KB) {
+    const int lim = kleft - KB * 32 - 4 * hi;   // one lane value against immediates
 #pragma unroll
-      for (int r = 0; r < 16; ++r)
-        if (KB * 32 + 8 * (r >> 2) + 4 * hi + (r & 3) >= kleft) sc[r] = -INFINITY;
-    }
-    u32x4 pf[2];
+    for (int r = 0; r < 16; ++r)
+      if (8 * (r >> 2) + (r & 3) >= lim) sc[r] = -INFINITY;
+  };
+  // P (packed for the PV MFMA) and the lane's sum of one 32-key step; the rare exact rescale
+  // (QL2E: always on the first step, m = 0 being no running max)
+  auto softmax = [&](const f32x16& sc, bool first, u32x4 (&pf)[2]) -> float {
     float rs = 0.f;
 #pragma unroll
     for (int hf = 0; hf < 2; ++hf) {
@@ -597,8 +600,6 @@ __global__ __launch_bounds__(256, 4) void attn_long_dma_kernel(const u16* qkv, i
       }
       pf[hf] = u32x4{pack2<BF>(p[0], p[1]), pack2<BF>(p[2], p[3]), pack2<BF>(p[4], p[5]), pack2<BF>(p[6], p[7])};
     }
-    // rare: rescale to the exact running max, recompute P. QL2E: the first step always rescales
-    // (m = 0 is no running max: its probabilities could all underflow)
     if ((QL2E && first) || __any(!(rs <= RS_MAX))) {
       float tmax = sc[0];
 #pragma unroll
@@ -636,7 +637,12 @@ __global__ __launch_bounds__(256, 4) void attn_long_dma_kernel(const u16* qkv, i
         pf[hf] = u32x4{pack2<BF>(p[0], p[1]), pack2<BF>(p[2], p[3]), pack2<BF>(p[4], p[5]), pack2<BF>(p[6], p[7])};
       }
     }
-    l += rs;
+    return rs;
+  };
+  // O^T += V^T P^T for keys KB * 32 .. of the tile in buffer BUF
+  auto pv = [&](auto bufc, auto kbc, const u32x4 (&pf)[2]) {
+    constexpr int BUF = decltype(bufc)::value, KB = decltype(kbc)::value;
+    constexpr int VOFF = BUF * 16384 + 8192 + KB * 32 * 128;
     {
       u32x4 v0 = v_frag32v<VOFF>(va0), v1 = v_frag32v<VOFF>(va1);
       lds_wait(v0, v1);
@@ -651,6 +657,9 @@ __global__ __launch_bounds__(256, 4) void attn_long_dma_kernel(const u16* qkv, i
     }
   };
   const int nkt = (T + 63) / 64;
+  // one 64-key tile: two 32-key steps. (Software-pipelined -- both QK chains first, the second
+  // under the first step's softmax -- needs 160 VGPRs, i.e. 3 waves per SIMD: 6.03 vs 5.31 ms of
+  // L/14 attention per step, profiles/r05_v6_attn_ab.txt.)
   auto tile = [&](int kt, auto bufc) {
     constexpr int BUF = decltype(bufc)::value;
     // this wave's pieces of tile kt landed; then every wave's, and every wave is done with tile
@@ -659,8 +668,18 @@ __global__ __launch_bounds__(256, 4) void attn_long_dma_kernel(const u16* qkv, i
     if (kt + 1 < nkt) issue(kt + 1, IC<1 - BUF>{});
     if (!active) return;
     const int kleft = T - kt * 64;   // valid keys in this tile (>= 1)
-    half(kt, kleft, bufc, IC<0>{});
-    if (kleft > 32) half(kt, kleft, bufc, IC<1>{});
+    f32x16 sc;
+    u32x4 pf[2];
+    qk(bufc, IC<0>{}, sc);
+    if (kleft < 32) mask(sc, kleft, 0);
+    l += softmax(sc, kt == 0, pf);
+    pv(bufc, IC<0>{}, pf);
+    if (kleft > 32) {
+      qk(bufc, IC<1>{}, sc);
+      if (kleft < 64) mask(sc, kleft, 1);
+      l += softmax(sc, false, pf);
+      pv(bufc, IC<1>{}, pf);
+    }
   };
   issue(0, IC<0>{});
   for (int kt = 0; kt < nkt; kt += 2) {
