@@ -1894,13 +1894,18 @@ static int search_bounded(clm_index* x, bool sampled, int64_t S, const u16* q16,
   // QPS, profiles/r04_v7_search_qb_ab.txt), and the blocks are balanced (a cap of 4096 gives
   // 10 k = 3392 + 3392 + 3216 instead of 4096 + 4096 + 1808)
   static const int64_t qb_cap = getenv("CLM_SEARCH_QB") ? std::max<int64_t>(64, atoll(getenv("CLM_SEARCH_QB"))) : 2560;
+  // the sample-score rows' stride: S (a multiple of 256 floats, 1 KB) plus 256 B, so the score
+  // GEMM's 16-row column stores do not land every row at the same power-of-two address offset
+  // ($CLM_SAMPLE_PAD floats, A/B)
+  static const int64_t spad = getenv("CLM_SAMPLE_PAD") ? atoll(getenv("CLM_SAMPLE_PAD")) : 64;
+  const int64_t ldS = S + spad;
   int64_t nqb = std::min<int64_t>(nq, qb_cap);
   if (sampled) {
     size_t fr = 0, tot = 0;
     int64_t cap_b = ws_mb << 20;
     if (hipMemGetInfo(&fr, &tot) == hipSuccess) cap_b = std::min<int64_t>(cap_b, (int64_t)(fr / 4));
     else (void)hipGetLastError();
-    nqb = std::min<int64_t>(std::min<int64_t>(nq, qb_cap), std::max<int64_t>(256, cap_b / ((int64_t)S * 4)));
+    nqb = std::min<int64_t>(std::min<int64_t>(nq, qb_cap), std::max<int64_t>(256, cap_b / (ldS * 4)));
   }
   {   // balance: the same number of blocks, equal sizes (multiples of 64 rows while that stays <= the cap)
     const int64_t nblk = (nq + nqb - 1) / nqb;
@@ -1909,12 +1914,12 @@ static int search_bounded(clm_index* x, bool sampled, int64_t S, const u16* q16,
   }
   size_t off = 0;
   auto take = [&](size_t bytes) { size_t o = off; off = round_up(off + bytes, 256); return o; };
-  const size_t o_sc = sampled ? take((size_t)nqb * S * 4) : 0;
+  const size_t o_sc = sampled ? take((size_t)nqb * ldS * 4) : 0;
   const size_t o_ts = take((size_t)nqb * k * 4);
   const size_t o_ti = take((size_t)nqb * k * 8);
   const size_t o_th = take((size_t)nq * 4);   // every query's threshold (the overflow pass reuses them)
-  const size_t o_cnt = take((size_t)nqb * 4);
-  const size_t o_est = take((size_t)nqb * 4);
+  const size_t o_cnt = take((size_t)nq * 4);   // every query's candidate count (read once, after the last block)
+  const size_t o_est = take((size_t)nq * 4);
   const size_t o_cs = take((size_t)nqb * CAND_CAP * 4);
   const size_t o_ci = take((size_t)nqb * CAND_CAP * 8);
   if ((r = grow(&x->ws2, &x->ws2_bytes, off))) return r;
@@ -1931,43 +1936,53 @@ static int search_bounded(clm_index* x, bool sampled, int64_t S, const u16* q16,
   const void* xrows = x->rows32 ? (const void*)x->rows32 : (const void*)x->rows;
   std::vector<int> hcnt;
   std::vector<int64_t> overflow, ocount;
+  // Phase 1, every block: the per-query thresholds (and, sampled, the estimated candidate counts)
+  // -- no host round trip between blocks
   for (int64_t q0 = 0; q0 < nq; q0 += nqb) {
     const int64_t nb = std::min(nqb, nq - q0);
-    // Filter tile for this block, from the block's own data: when most of its queries' candidate
-    // windows hold more than CAND_CAP rows (near-duplicate rows: the sampled count above the
-    // threshold, scaled by N / S), the appends dominate the pass and gemm_kernel's 256 x 256 FILTER
-    // epilogue is the faster one; otherwise G2's 256 x 192 (same candidates either way)
-    bool dense = false;
     if (sampled) {
       GemmArgs ga{};
       ga.A = q16 + q0 * dim; ga.lda = dim; ga.W = x->samp; ga.ldw = dim;
-      ga.M = (int)nb; ga.N = (int)S; ga.K = dim; ga.out = sc; ga.ldo = S;
+      ga.M = (int)nb; ga.N = (int)S; ga.K = dim; ga.out = sc; ga.ldo = ldS;
       ga.rscale = qinv + q0; ga.cscale = x->samp_inv;
       KCHK(gemm(false, EPI_SCORE, ga, st));
       if (k <= 8 && !g_kth_radix) {   // one streaming pass for the k-th value alone
-        KCHK(kth_thresholds(sc, S, nb, S, k, RESCORE_MARGIN, th + q0, st));
+        KCHK(kth_thresholds(sc, ldS, nb, S, k, RESCORE_MARGIN, th + q0, st));
       } else {
-        KCHK(topk_rows(sc, S, nb, S, k, 0, ts, ti, k, st));
+        KCHK(topk_rows(sc, ldS, nb, S, k, 0, ts, ti, k, st));
         KCHK(filter_thresholds(ts, k, nb, k, RESCORE_MARGIN, th + q0, st));
       }
-      KCHK(count_ge(sc, S, nb, S, th + q0, est, st));
-      hest.resize(nb);
-      HIPCHK(hipMemcpyAsync(hest.data(), est, (size_t)nb * 4, hipMemcpyDeviceToHost, st));
-      HIPCHK(hipStreamSynchronize(st));
-      int64_t over = 0;
-      for (int64_t i = 0; i < nb; ++i) over += (double)hest[i] * ((double)N / (double)S) > CAND_CAP;
-      dense = 2 * over > nb;
+      KCHK(count_ge(sc, ldS, nb, S, th + q0, est + q0, st));
     } else {
       if ((r = search_scan(x, false, q16 + q0 * dim, qinv + q0, nullptr, nullptr, nb, k, ts, ti, st))) return r;
       KCHK(filter_thresholds(ts, k, nb, k, RESCORE_MARGIN, th + q0, st));
     }
-    HIPCHK(hipMemsetAsync(cnt, 0, (size_t)nb * 4, st));
+  }
+  // Filter tile per block, from the block's own data: when most of its queries' candidate windows
+  // hold more than CAND_CAP rows (near-duplicate rows: the sampled count above the threshold,
+  // scaled by N / S), the appends dominate the pass and gemm_kernel's 256 x 256 FILTER epilogue is
+  // the faster one; otherwise G2's 256 x 192 (same candidates either way)
+  if (sampled) {
+    hest.resize(nq);
+    HIPCHK(hipMemcpyAsync(hest.data(), est, (size_t)nq * 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+  }
+  HIPCHK(hipMemsetAsync(cnt, 0, (size_t)nq * 4, st));
+  // Phase 2, every block: the filter pass and the exact re-score of its candidates
+  for (int64_t q0 = 0; q0 < nq; q0 += nqb) {
+    const int64_t nb = std::min(nqb, nq - q0);
+    bool dense = false;
+    if (sampled) {
+      int64_t over = 0;
+      for (int64_t i = 0; i < nb; ++i) over += (double)hest[q0 + i] * ((double)N / (double)S) > CAND_CAP;
+      dense = 2 * over > nb;
+    }
     GemmArgs gf{};
     gf.A = q16 + q0 * dim; gf.lda = dim; gf.W = x->rows; gf.ldw = dim;
     gf.M = (int)nb; gf.N = (int)N; gf.K = dim;
     gf.rscale = qinv + q0; gf.cscale = x->inv;
     gf.theta = th + q0; gf.theta_ld = 1;
-    gf.cnt = cnt; gf.cand_s = cs; gf.cand_i = ci; gf.cap = CAND_CAP; gf.base = x->offset;
+    gf.cnt = cnt + q0; gf.cand_s = cs; gf.cand_i = ci; gf.cap = CAND_CAP; gf.base = x->offset;
     gf.m_fastest = 1;
     gf.cbound = inv_keys_of(x, st);
     // never clm_debug_set / $CLM_GEMM_DEBUG (those drop epilogues: the candidate lists would be
@@ -1978,17 +1993,17 @@ static int search_bounded(clm_index* x, bool sampled, int64_t S, const u16* q16,
     static const bool cfg_forced = getenv("CLM_GEMM_CFG") != nullptr;
     KCHK(gemm_cfg(false, EPI_FILTER, dense && !cfg_forced ? 1 : -1, gf, st));
     x->search_stats[dense ? 5 : 4] += nb;
-    KCHK(rescore_select(cs, ci, cnt, CAND_CAP, q32 + q0 * dim, qn + q0, dim, xrows, !x->rows32, x->offset,
+    KCHK(rescore_select(cs, ci, cnt + q0, CAND_CAP, q32 + q0 * dim, qn + q0, dim, xrows, !x->rows32, x->offset,
                         RESCORE_MARGIN, nb, k, osc + q0 * k, oix + q0 * k, st));
-    hcnt.resize(nb);
-    HIPCHK(hipMemcpyAsync(hcnt.data(), cnt, (size_t)nb * 4, hipMemcpyDeviceToHost, st));
-    HIPCHK(hipStreamSynchronize(st));
-    for (int64_t i = 0; i < nb; ++i)
-      if (hcnt[i] > CAND_CAP) {
-        overflow.push_back(q0 + i);
-        ocount.push_back(hcnt[i]);
-      }
   }
+  hcnt.resize(nq);
+  HIPCHK(hipMemcpyAsync(hcnt.data(), cnt, (size_t)nq * 4, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
+  for (int64_t i = 0; i < nq; ++i)
+    if (hcnt[i] > CAND_CAP) {
+      overflow.push_back(i);
+      ocount.push_back(hcnt[i]);
+    }
   x->search_stats[sampled ? 0 : 3] += nq - (int64_t)overflow.size();
   if (overflow.empty()) return CLM_OK;
   // Candidate lists beyond CAND_CAP (near-duplicate rows inside the window). Lists of up to

@@ -402,11 +402,26 @@ __global__ __launch_bounds__(256) void kth_threshold_kernel(const float* S, int6
   if ((lds & 3) == 0 && ((uintptr_t)S & 15) == 0) {
     const int64_t C4 = C >> 2;
     const float4* s4 = (const float4*)s;
-    for (int64_t i = tid; i < C4; i += 256) {
+    int64_t i = tid;
+    for (; i + 768 < C4; i += 1024) {   // four 16-B loads in flight before the inserts
+      const float4 a = s4[i], b = s4[i + 256], c = s4[i + 512], e = s4[i + 768];
+      // a block whose 16 values are all below the current 8th largest is one test, no inserts
+      // (NaN-propagating maximum: a block holding a NaN takes the per-value path, as the plain loop)
+      auto mx2 = [](float x, float y) { return __builtin_elementwise_maximum(x, y); };
+      const float mx = mx2(mx2(mx2(mx2(a.x, a.y), mx2(a.z, a.w)), mx2(mx2(b.x, b.y), mx2(b.z, b.w))),
+                           mx2(mx2(mx2(c.x, c.y), mx2(c.z, c.w)), mx2(mx2(e.x, e.y), mx2(e.z, e.w))));
+      if (!(mx == mx) || fkey(mx) > t[KTH_MAX - 1]) {
+        insert(fkey(a.x)); insert(fkey(a.y)); insert(fkey(a.z)); insert(fkey(a.w));
+        insert(fkey(b.x)); insert(fkey(b.y)); insert(fkey(b.z)); insert(fkey(b.w));
+        insert(fkey(c.x)); insert(fkey(c.y)); insert(fkey(c.z)); insert(fkey(c.w));
+        insert(fkey(e.x)); insert(fkey(e.y)); insert(fkey(e.z)); insert(fkey(e.w));
+      }
+    }
+    for (; i < C4; i += 256) {
       const float4 v = s4[i];
       insert(fkey(v.x)); insert(fkey(v.y)); insert(fkey(v.z)); insert(fkey(v.w));
     }
-    for (int64_t i = (C4 << 2) + tid; i < C; i += 256) insert(fkey(s[i]));
+    for (int64_t j = (C4 << 2) + tid; j < C; j += 256) insert(fkey(s[j]));
   } else {
     for (int64_t i = tid; i < C; i += 256) insert(fkey(s[i]));
   }
@@ -683,7 +698,23 @@ __global__ __launch_bounds__(256) void count_ge_kernel(const float* S, int64_t l
   const float t = th[row];
   const float* s = S + row * lds;
   int c = 0;
-  for (int64_t j = threadIdx.x; j < C; j += 256) c += s[j] >= t;
+  if ((lds & 3) == 0 && ((uintptr_t)S & 15) == 0) {   // 16-B loads, four in flight per thread
+    const int64_t C4 = C >> 2;
+    const float4* s4 = (const float4*)s;
+    int64_t i = threadIdx.x;
+    for (; i + 768 < C4; i += 1024) {
+      const float4 a = s4[i], b = s4[i + 256], d = s4[i + 512], e = s4[i + 768];
+      c += (a.x >= t) + (a.y >= t) + (a.z >= t) + (a.w >= t) + (b.x >= t) + (b.y >= t) + (b.z >= t) + (b.w >= t) +
+           (d.x >= t) + (d.y >= t) + (d.z >= t) + (d.w >= t) + (e.x >= t) + (e.y >= t) + (e.z >= t) + (e.w >= t);
+    }
+    for (; i < C4; i += 256) {
+      const float4 a = s4[i];
+      c += (a.x >= t) + (a.y >= t) + (a.z >= t) + (a.w >= t);
+    }
+    for (int64_t j = (C4 << 2) + threadIdx.x; j < C; j += 256) c += s[j] >= t;
+  } else {
+    for (int64_t j = threadIdx.x; j < C; j += 256) c += s[j] >= t;
+  }
   for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
   if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = c;
   __syncthreads();
