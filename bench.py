@@ -511,8 +511,8 @@ def newest_profile(pattern: str):
     import glob
     best, key = None, None
     for f in glob.glob(os.path.join(REPO, "profiles", f"*_{pattern}")):
-        m = re.match(r"r(\d+)_v(\d+)", os.path.basename(f))
-        if not m:
+        m = re.fullmatch(r"r(\d+)_v(\d+)_" + re.escape(pattern), os.path.basename(f))
+        if not m:   # e.g. r05_v5_attn_pmc_summary.json is not a "pmc_summary.json"
             continue
         kk = (int(m.group(1)), int(m.group(2)))
         if key is None or kk > key:
