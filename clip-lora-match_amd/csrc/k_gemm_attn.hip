@@ -35,16 +35,23 @@ constexpr int FA_SEC = FA_BM * 128;    // one staged section (q, k or v): [256 r
 static_assert(3 * FA_SEC <= FA_LDS, "q/k/v staging must fit in the ring's LDS");
 static_assert(FA_BM % (8 * FA_NW) == 0 && FA_BN % (8 * FA_NW) == 0, "rows split evenly over waves");
 
-// V^T operand of O^T = V^T P^T from the staged V section (rows = tile rows, 16-B chunks XOR-
-// swizzled by (row >> 1) & 7): k_attn.hip's v_frag_trT on absolute tile rows, clamped to the
-// image (a clamped row only ever meets a masked key, whose P is exactly 0)
+// The staged q / k / v sections ([256 rows][128 B]) swizzle their 16-B chunks by row & 7 (the
+// DMA ring's (row >> 1) & 7 pairs rows 2j and 2j + 1 on one chunk): 8 consecutive rows then hold a
+// chunk at 8 distinct positions, so the 16-B staging writes (8-lane groups of consecutive rows),
+// the q / k fragment reads (ds_read_b128 at any sequence offset) and the transposed V reads
+// (32 lanes = 8 consecutive rows x 2 chunks x 2 halves) are all bank-conflict free.
+__device__ __forceinline__ int swz_s(int row, int chunk) { return chunk ^ (row & 7); }
+
+// V^T operand of O^T = V^T P^T from the staged V section (rows = tile rows): k_attn.hip's
+// v_frag_trT on absolute tile rows, clamped to the image (a clamped row only ever meets a masked
+// key, whose P is exactly 0)
 __device__ __forceinline__ u32x4 v_frag_rows(const uint8_t* sec, int kbase, int nb, int lane) {
   typedef short s16x4 __attribute__((ext_vector_type(4)));
   const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
   const int chunk = nb * 2 + (p >> 1);
   const int ka = min(kbase + g * 4 + q, FA_BM - 1), kb = min(kbase + 16 + g * 4 + q, FA_BM - 1);
-  const uint8_t* pa = sec + ka * 128 + ((chunk ^ ((ka >> 1) & 7)) << 4) + (p & 1) * 8;
-  const uint8_t* pb = sec + kb * 128 + ((chunk ^ ((kb >> 1) & 7)) << 4) + (p & 1) * 8;
+  const uint8_t* pa = sec + ka * 128 + (swz_s(ka, chunk) << 4) + (p & 1) * 8;
+  const uint8_t* pb = sec + kb * 128 + (swz_s(kb, chunk) << 4) + (p & 1) * 8;
   const s16x4 ra = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)pa);
   const s16x4 rb = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)pb);
   const u32x2 x = __builtin_bit_cast(u32x2, ra), y = __builtin_bit_cast(u32x2, rb);
@@ -166,16 +173,24 @@ __device__ __forceinline__ void gemm_attn_body(const FaArgs& a, int bid, int nwg
   // lane holds row wm*64 + mb*16 + (lane & 15), columns wn*96 + nb*16 + 4g .. +3 of the tile:
   // section (q, k, v) = column / 64, head dim = column % 64
   lds_barrier();   // every wave has read its last fragments out of the ring
+  // 16-B writes: v_permlane16_swap trades the odd 16-lane groups' block-nb words with the even
+  // groups' block-(nb + 1) words, so lane group q holds the 8 consecutive columns
+  // (nb + (q & 1)) * 16 + (q >> 1) * 8 .. + 7 of its row (one chunk of one section)
+  static_assert(FA_TN % 2 == 0, "column blocks are swapped in pairs");
 #pragma unroll
   for (int mb = 0; mb < FA_TM; ++mb) {
     const int row = wm * (FA_BM / FA_WM) + mb * 16 + (lane & 15);
 #pragma unroll
-    for (int nb = 0; nb < FA_TN; ++nb) {
-      const int col = wn * (FA_BN / FA_WN) + nb * 16 + 4 * g;
+    for (int nb = 0; nb < FA_TN; nb += 2) {
+      const u32x2 p0{pack2<BF>(acc[mb][nb][0] + bv[nb].x, acc[mb][nb][1] + bv[nb].y),
+                     pack2<BF>(acc[mb][nb][2] + bv[nb].z, acc[mb][nb][3] + bv[nb].w)};
+      const u32x2 p1{pack2<BF>(acc[mb][nb + 1][0] + bv[nb + 1].x, acc[mb][nb + 1][1] + bv[nb + 1].y),
+                     pack2<BF>(acc[mb][nb + 1][2] + bv[nb + 1].z, acc[mb][nb + 1][3] + bv[nb + 1].w)};
+      const auto rx = __builtin_amdgcn_permlane16_swap(p0.x, p1.x, false, false);
+      const auto ry = __builtin_amdgcn_permlane16_swap(p0.y, p1.y, false, false);
+      const int col = wn * (FA_BN / FA_WN) + (nb + (g & 1)) * 16 + (g >> 1) * 8;
       const int dim = col & 63;
-      const u32x2 v{pack2<BF>(acc[mb][nb][0] + bv[nb].x, acc[mb][nb][1] + bv[nb].y),
-                    pack2<BF>(acc[mb][nb][2] + bv[nb].z, acc[mb][nb][3] + bv[nb].w)};
-      *(u32x2*)(smem + (col >> 6) * FA_SEC + row * 128 + (swz(row, dim >> 3) << 4) + (dim & 7) * 2) = v;
+      *(u32x4*)(smem + (col >> 6) * FA_SEC + row * 128 + (swz_s(row, dim >> 3) << 4)) = u32x4{rx[0], ry[0], rx[1], ry[1]};
     }
   }
   lds_barrier();
@@ -210,7 +225,7 @@ __device__ __forceinline__ void gemm_attn_body(const FaArgs& a, int bid, int nwg
     {
       const int qrow = r0 + min(qi, T - 1);
 #pragma unroll
-      for (int kk = 0; kk < 2; ++kk) qa[kk] = *(const u32x4*)(sQ + qrow * 128 + swz(qrow, kk * 4 + g) * 16);
+      for (int kk = 0; kk < 2; ++kk) qa[kk] = *(const u32x4*)(sQ + qrow * 128 + swz_s(qrow, kk * 4 + g) * 16);
     }
     const int nkt = CAUSAL ? min((q0 + 15) / 64 + 1, ntiles) : ntiles;
     f32x4 sc[2][4];   // S^T: lane holds query qi, keys kt*64 + nb*16 + 4g + 0..3
@@ -225,7 +240,7 @@ __device__ __forceinline__ void gemm_attn_body(const FaArgs& a, int bid, int nwg
 #pragma unroll
         for (int kk = 0; kk < 2; ++kk) {
           const int c = kk * 4 + g;
-          sc[kt][nb] = mfma16<BF>(*(const u32x4*)(sK + krow * 128 + swz(krow, c) * 16), qa[kk], sc[kt][nb]);
+          sc[kt][nb] = mfma16<BF>(*(const u32x4*)(sK + krow * 128 + swz_s(krow, c) * 16), qa[kk], sc[kt][nb]);
         }
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
