@@ -808,8 +808,12 @@ int attn_long_mode() {
 }
 }  // namespace
 
+// attn_long_dma_kernel's per-tile buffer resources take 32-bit byte offsets over a sequence's
+// rows: sequences up to 65,535 tokens (rows of <= 3 x 1024 16-bit values: < 2^31 bytes)
+constexpr int ATTN_DMA_MAX_T = 65535;
+
 bool attention_folds_log2e(bool bf16, bool causal, int T) {
-  return bf16 && !causal && T > 128 && attn_long_mode() == 3;
+  return bf16 && !causal && T > 128 && T <= ATTN_DMA_MAX_T && attn_long_mode() == 3;
 }
 
 hipError_t attention(bool bf16, bool causal, const u16* qkv, int64_t ldq, u16* out, int64_t ldo, int B, int T,
@@ -833,7 +837,9 @@ hipError_t attention(bool bf16, bool causal, const u16* qkv, int64_t ldq, u16* o
 #undef CLM_SMALL
     return hipGetLastError();
   }
-  const int long_mode = attn_long_mode();
+  // longer sequences than the DMA kernel's offsets cover take the SUB32 register-staged kernel
+  const int long_mode = (attn_long_mode() == 3 && (T > ATTN_DMA_MAX_T || (int64_t)T * ldq * 2 >= (1ll << 31)))
+                            ? 2 : attn_long_mode();
   if (!causal && long_mode) {
     const int nqb = (T + 127) / 128;
     const int64_t nwg = (int64_t)nqb * H * B;
