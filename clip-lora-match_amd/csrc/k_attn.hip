@@ -840,6 +840,7 @@ hipError_t attention(bool bf16, bool causal, const u16* qkv, int64_t ldq, u16* o
   // longer sequences than the DMA kernel's offsets cover take the SUB32 register-staged kernel
   const int long_mode = (attn_long_mode() == 3 && (T > ATTN_DMA_MAX_T || (int64_t)T * ldq * 2 >= (1ll << 31)))
                             ? 2 : attn_long_mode();
+  if (q_log2e && long_mode != 3) return hipErrorInvalidValue;   // only that kernel takes log2-domain q
   if (!causal && long_mode) {
     const int nqb = (T + 127) / 128;
     const int64_t nwg = (int64_t)nqb * H * B;
