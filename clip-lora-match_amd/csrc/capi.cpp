@@ -1914,7 +1914,12 @@ static int search_bounded(clm_index* x, bool sampled, int64_t S, const u16* q16,
   }
   size_t off = 0;
   auto take = [&](size_t bytes) { size_t o = off; off = round_up(off + bytes, 256); return o; };
-  const size_t o_sc = sampled ? take((size_t)nqb * ldS * 4) : 0;
+  // fp16 sample scores (rounded toward -inf: the k-th largest over them is <= the fp32 one, so
+  // the thresholds only widen) where the one-pass k-th value path runs: half the bytes of the
+  // phase's three passes ($CLM_SAMPLE_F32=1: fp32, A/B)
+  static const bool s32_env = getenv("CLM_SAMPLE_F32") && atoi(getenv("CLM_SAMPLE_F32")) != 0;
+  const bool s16 = sampled && k <= 8 && !g_kth_radix && !s32_env;
+  const size_t o_sc = sampled ? take((size_t)nqb * ldS * (s16 ? 2 : 4)) : 0;
   const size_t o_ts = take((size_t)nqb * k * 4);
   const size_t o_ti = take((size_t)nqb * k * 8);
   const size_t o_th = take((size_t)nq * 4);   // every query's threshold (the overflow pass reuses them)
@@ -1943,16 +1948,21 @@ static int search_bounded(clm_index* x, bool sampled, int64_t S, const u16* q16,
     if (sampled) {
       GemmArgs ga{};
       ga.A = q16 + q0 * dim; ga.lda = dim; ga.W = x->samp; ga.ldw = dim;
-      ga.M = (int)nb; ga.N = (int)S; ga.K = dim; ga.out = sc; ga.ldo = ldS;
+      ga.M = (int)nb; ga.N = (int)S; ga.K = dim; ga.out = sc; ga.ldo = ldS; ga.out16 = s16 ? 1 : 0;
       ga.rscale = qinv + q0; ga.cscale = x->samp_inv;
       KCHK(gemm(false, EPI_SCORE, ga, st));
-      if (k <= 8 && !g_kth_radix) {   // one streaming pass for the k-th value alone
-        KCHK(kth_thresholds(sc, ldS, nb, S, k, RESCORE_MARGIN, th + q0, st));
+      if (s16) {
+        KCHK(kth_thresholds16((const u16*)sc, ldS, nb, S, k, RESCORE_MARGIN, th + q0, st));
+        KCHK(count_ge16((const u16*)sc, ldS, nb, S, th + q0, est + q0, st));
       } else {
-        KCHK(topk_rows(sc, ldS, nb, S, k, 0, ts, ti, k, st));
-        KCHK(filter_thresholds(ts, k, nb, k, RESCORE_MARGIN, th + q0, st));
+        if (k <= 8 && !g_kth_radix) {   // one streaming pass for the k-th value alone
+          KCHK(kth_thresholds(sc, ldS, nb, S, k, RESCORE_MARGIN, th + q0, st));
+        } else {
+          KCHK(topk_rows(sc, ldS, nb, S, k, 0, ts, ti, k, st));
+          KCHK(filter_thresholds(ts, k, nb, k, RESCORE_MARGIN, th + q0, st));
+        }
+        KCHK(count_ge(sc, ldS, nb, S, th + q0, est + q0, st));
       }
-      KCHK(count_ge(sc, ldS, nb, S, th + q0, est + q0, st));
     } else {
       if ((r = search_scan(x, false, q16 + q0 * dim, qinv + q0, nullptr, nullptr, nb, k, ts, ti, st))) return r;
       KCHK(filter_thresholds(ts, k, nb, k, RESCORE_MARGIN, th + q0, st));

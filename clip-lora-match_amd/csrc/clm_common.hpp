@@ -99,6 +99,15 @@ __device__ __forceinline__ float wave_max(float v) { return wave_reduce<true>(v)
 __device__ __forceinline__ float group16_sum(float v) { return row16_reduce<false>(v); }
 __device__ __forceinline__ float group16_max(float v) { return row16_reduce<true>(v); }
 
+// fp16 bits of the largest fp16 value <= v (round toward -inf; NaN stays NaN): RNE, then one
+// step down when that rounded up
+__device__ __forceinline__ uint32_t f16_down(float v) {
+  const _Float16 h = (_Float16)v;
+  uint32_t b = __builtin_bit_cast(uint16_t, h);
+  if ((float)h > v) b = b == 0u ? 0x8001u : (b & 0x8000u) ? b + 1u : b - 1u;
+  return b;
+}
+
 __device__ __forceinline__ float quick_gelu(float x) {
   // TF/activations.py:123  x * sigmoid(1.702 x), as x * rcp(1 + 2^(-1.702 log2(e) x)):
   // v_exp_f32 + v_rcp_f32 (1 ulp) instead of an IEEE division (4 v_div_* + v_fma per value,

@@ -83,7 +83,11 @@ __device__ __forceinline__ void epilogue_scalar(const GemmArgs& g, const f32x4 (
         else if constexpr (epi_gelu(EPI)) ((u16*)g.out)[(int64_t)m * g.ldo + nj] = from_f32<BF>(quick_gelu(x));
         else if constexpr (EPI == EPI_RESID) ((float*)g.out)[(int64_t)m * g.ldo + nj] += x;
         else if constexpr (EPI == EPI_PATCH) ((float*)g.out)[prow * g.ldo + nj] = x + aux[nj];
-        else if constexpr (EPI == EPI_SCORE) ((float*)g.out)[(int64_t)m * g.ldo + nj] = x * rs * (g.cscale ? g.cscale[nj] : 1.f);
+        else if constexpr (EPI == EPI_SCORE) {
+          const float v = x * rs * (g.cscale ? g.cscale[nj] : 1.f);
+          if (g.out16) ((u16*)g.out)[(int64_t)m * g.ldo + nj] = (u16)f16_down(v);
+          else ((float*)g.out)[(int64_t)m * g.ldo + nj] = v;
+        }
         else {
           const float sc = x * rs * g.cscale[nj];
           if (sc >= g.theta[(int64_t)m * g.theta_ld]) {
@@ -284,6 +288,23 @@ __device__ __forceinline__ void epilogue(const GemmArgs& g, const f32x4 (&acc)[B
       if constexpr (EPI == EPI_FILTER) th[mb] = m < g.M ? g.theta[(int64_t)m * g.theta_ld] : 0.f;
     }
     if constexpr (EPI == EPI_SCORE) {
+      if (g.out16) {   // fp16 scores rounded toward -inf, 8 B per lane and block
+        const auto oh = buf_rsrc((const u16*)g.out + out_off + (int64_t)m0 * g.ldo, nrec);
+#pragma unroll
+        for (int mb = 0; mb < C::TM; ++mb) {
+          const int m = wrow + mb * 16;
+#pragma unroll
+          for (int nb = 0; nb < C::TN; ++nb) {
+            const int n = wcol + nb * 16;
+            const float4 c = cv[nb];
+            const uint32_t off = (m < g.M && n < g.N) ? (uint32_t)(((int64_t)(m - m0) * g.ldo + n) * 2) : BUF_OOB;
+            const uint32_t h0 = f16_down(acc[mb][nb][0] * rs[mb] * c.x), h1 = f16_down(acc[mb][nb][1] * rs[mb] * c.y);
+            const uint32_t h2 = f16_down(acc[mb][nb][2] * rs[mb] * c.z), h3 = f16_down(acc[mb][nb][3] * rs[mb] * c.w);
+            __builtin_amdgcn_raw_buffer_store_b64(u32x2{h0 | (h1 << 16), h2 | (h3 << 16)}, oh, off, 0, 0);
+          }
+        }
+        return;
+      }
       const auto ob = buf_rsrc((const float*)g.out + out_off + (int64_t)m0 * g.ldo, nrec);
 #pragma unroll
       for (int mb = 0; mb < C::TM; ++mb) {

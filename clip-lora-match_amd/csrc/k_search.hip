@@ -384,10 +384,14 @@ __device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
   for (int o = 32; o > 0; o >>= 1) v = max(v, (uint32_t)__shfl_xor((int)v, o));
   return v;
 }
-__global__ __launch_bounds__(256) void kth_threshold_kernel(const float* S, int64_t lds, int64_t C, int k, float margin,
+// H16: fp16 score rows (GemmArgs::out16), 8 values per 16-B load; fkey of the value widened to
+// fp32 (exact), so the keys order as the fp16 values do
+template <bool H16>
+__global__ __launch_bounds__(256) void kth_threshold_kernel(const void* Sv, int64_t lds, int64_t C, int k, float margin,
                                                             float* th) {
   __shared__ uint32_t part[4 * KTH_MAX];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const float* S = (const float*)Sv;
   const float* s = S + (int64_t)blockIdx.x * lds;
   uint32_t t[KTH_MAX];
 #pragma unroll
@@ -399,7 +403,37 @@ __global__ __launch_bounds__(256) void kth_threshold_kernel(const float* S, int6
     for (int j = KTH_MAX - 1; j > 0; --j)
       if (t[j] > t[j - 1]) { const uint32_t a = t[j]; t[j] = t[j - 1]; t[j - 1] = a; }
   };
-  if ((lds & 3) == 0 && ((uintptr_t)S & 15) == 0) {
+  if constexpr (H16) {   // the caller checked lds % 8 == 0 and 16-B alignment
+    const u16* sh = (const u16*)Sv + (int64_t)blockIdx.x * lds;
+    const int64_t C8 = C >> 3;
+    const u32x4* s8 = (const u32x4*)sh;
+    auto hv = [](uint32_t w, int hi) {
+      return (float)__builtin_bit_cast(_Float16, (uint16_t)(hi ? (w >> 16) : (w & 0xFFFFu)));
+    };
+    int64_t i = tid;
+    for (; i + 256 < C8; i += 512) {   // two 16-B loads (16 values) in flight before the inserts
+      const u32x4 a = s8[i], b = s8[i + 256];
+      float v[16];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        v[2 * j] = hv(a[j], 0); v[2 * j + 1] = hv(a[j], 1);
+        v[8 + 2 * j] = hv(b[j], 0); v[9 + 2 * j] = hv(b[j], 1);
+      }
+      float mx = v[0];
+#pragma unroll
+      for (int j = 1; j < 16; ++j) mx = __builtin_elementwise_maximum(mx, v[j]);
+      if (!(mx == mx) || fkey(mx) > t[KTH_MAX - 1]) {
+#pragma unroll
+        for (int j = 0; j < 16; ++j) insert(fkey(v[j]));
+      }
+    }
+    for (; i < C8; i += 256) {
+      const u32x4 a = s8[i];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) { insert(fkey(hv(a[j], 0))); insert(fkey(hv(a[j], 1))); }
+    }
+    for (int64_t j = (C8 << 3) + tid; j < C; j += 256) insert(fkey((float)__builtin_bit_cast(_Float16, sh[j])));
+  } else if ((lds & 3) == 0 && ((uintptr_t)S & 15) == 0) {
     const int64_t C4 = C >> 2;
     const float4* s4 = (const float4*)s;
     int64_t i = tid;
@@ -720,7 +754,47 @@ __global__ __launch_bounds__(256) void count_ge_kernel(const float* S, int64_t l
   __syncthreads();
   if (threadIdx.x == 0) cnt[row] = part[0] + part[1] + part[2] + part[3];
 }
+// fp16 score rows (GemmArgs::out16): 8 values per 16-B load
+__device__ __forceinline__ float f16v(uint32_t w, int hi) {
+  return (float)__builtin_bit_cast(_Float16, (uint16_t)(hi ? (w >> 16) : (w & 0xFFFFu)));
+}
+__global__ __launch_bounds__(256) void count_ge16_kernel(const u16* S, int64_t lds, int64_t C, const float* th,
+                                                         int* cnt) {
+  __shared__ int part[4];
+  const int64_t row = blockIdx.x;
+  const float t = th[row];
+  const u16* s = S + row * lds;
+  int c = 0;
+  const int64_t C8 = C >> 3;
+  const u32x4* s8 = (const u32x4*)s;
+  int64_t i = threadIdx.x;
+  for (; i + 256 < C8; i += 512) {
+    const u32x4 a = s8[i], b = s8[i + 256];
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      c += (f16v(a[j], 0) >= t) + (f16v(a[j], 1) >= t) + (f16v(b[j], 0) >= t) + (f16v(b[j], 1) >= t);
+  }
+  for (; i < C8; i += 256) {
+    const u32x4 a = s8[i];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) c += (f16v(a[j], 0) >= t) + (f16v(a[j], 1) >= t);
+  }
+  for (int64_t j = (C8 << 3) + threadIdx.x; j < C; j += 256)
+    c += (float)__builtin_bit_cast(_Float16, s[j]) >= t;
+  for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
+  if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = c;
+  __syncthreads();
+  if (threadIdx.x == 0) cnt[row] = part[0] + part[1] + part[2] + part[3];
+}
 }  // namespace
+
+hipError_t count_ge16(const u16* scores, int64_t lds, int64_t nq, int64_t C, const float* th, int* cnt,
+                      hipStream_t s) {
+  if (nq <= 0) return hipSuccess;
+  if ((lds & 7) || ((uintptr_t)scores & 15)) return hipErrorInvalidValue;
+  count_ge16_kernel<<<(unsigned)nq, 256, 0, s>>>(scores, lds, C, th, cnt);
+  return hipGetLastError();
+}
 
 hipError_t count_ge(const float* scores, int64_t lds, int64_t nq, int64_t C, const float* th, int* cnt, hipStream_t s) {
   if (nq <= 0) return hipSuccess;
@@ -837,7 +911,15 @@ hipError_t kth_thresholds(const float* scores, int64_t lds, int64_t nq, int64_t 
                           hipStream_t s) {
   if (nq <= 0) return hipSuccess;
   if (k < 1 || k > KTH_MAX || C < k) return hipErrorInvalidValue;
-  kth_threshold_kernel<<<(unsigned)nq, 256, 0, s>>>(scores, lds, C, k, margin, th);
+  kth_threshold_kernel<false><<<(unsigned)nq, 256, 0, s>>>(scores, lds, C, k, margin, th);
+  return hipGetLastError();
+}
+
+hipError_t kth_thresholds16(const u16* scores, int64_t lds, int64_t nq, int64_t C, int k, float margin, float* th,
+                            hipStream_t s) {
+  if (nq <= 0) return hipSuccess;
+  if (k < 1 || k > KTH_MAX || C < k || (lds & 7) || ((uintptr_t)scores & 15)) return hipErrorInvalidValue;
+  kth_threshold_kernel<true><<<(unsigned)nq, 256, 0, s>>>(scores, lds, C, k, margin, th);
   return hipGetLastError();
 }
 

@@ -38,6 +38,9 @@ struct GemmArgs {
   // split-K (gemm_kernel configs only, EPI_SCORE as the fp32 partial store): ksplit > 1 cuts K
   // into ksplit equal slices; slice s of every tile writes out + s * split_stride
   int ksplit; int64_t split_stride;
+  // EPI_SCORE: 1 = store the scores as fp16 rounded toward -inf (f16_down: never above the fp32
+  // score, so a k-th largest taken over them bounds the fp32 one from below), out as u16 [M, ldo]
+  int out16;
   // varlen rows (packed text tower): if set, the row count is *m_dev (device-resident, <= M, which
   // sizes the grid), so a captured graph replays with data-dependent row counts
   const int* m_dev;
@@ -202,6 +205,10 @@ hipError_t topk_any(const float* scores, int64_t lds, const int64_t* idx, int64_
                     int64_t base, float* out_s, int64_t* out_i, int64_t ldo, void* ws, hipStream_t s);
 // cnt[q] = number of scores in row q [C] (row stride lds) that are >= th[q]
 hipError_t count_ge(const float* scores, int64_t lds, int64_t nq, int64_t C, const float* th, int* cnt, hipStream_t s);
+// the same over fp16 scores (GemmArgs::out16 score matrices)
+hipError_t count_ge16(const u16* scores, int64_t lds, int64_t nq, int64_t C, const float* th, int* cnt, hipStream_t s);
+hipError_t kth_thresholds16(const u16* scores, int64_t lds, int64_t nq, int64_t C, int k, float margin, float* th,
+                            hipStream_t s);
 // merge `parts` candidate lists per row: in [nq, parts*k_in] -> out [nq, k]
 hipError_t topk_merge(const float* in_s, const int64_t* in_i, int64_t nq, int parts, int k_in,
                       int k, float* out_s, int64_t* out_i, hipStream_t s);
