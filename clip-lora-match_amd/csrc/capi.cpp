@@ -1919,7 +1919,15 @@ static int search_bounded(clm_index* x, bool sampled, int64_t S, const u16* q16,
   // phase's three passes ($CLM_SAMPLE_F32=1: fp32, A/B)
   static const bool s32_env = getenv("CLM_SAMPLE_F32") && atoi(getenv("CLM_SAMPLE_F32")) != 0;
   const bool s16 = sampled && k <= 8 && !g_kth_radix && !s32_env;
-  const size_t o_sc = sampled ? take((size_t)nqb * ldS * (s16 ? 2 : 4)) : 0;
+  // ... and stored as the maxima of groups of 4 sample rows (a subset of the scores: its k-th
+  // largest is at most theirs, so θ stays a lower bound; 4x fewer bytes again). The dense-tile
+  // estimate then counts groups, times 4 (an upper bound of the scores >= θ).
+  // ($CLM_SAMPLE_GROUP=0: every score, A/B)
+  static const bool grp_env = !(getenv("CLM_SAMPLE_GROUP") && atoi(getenv("CLM_SAMPLE_GROUP")) == 0);
+  const bool sgrp = s16 && grp_env && S % 256 == 0;
+  const int64_t Sc = sgrp ? S / 4 : S;             // stored values per sample-score row
+  const int64_t ldC = sgrp ? S / 4 + 64 : ldS;     // their row stride
+  const size_t o_sc = sampled ? take((size_t)nqb * ldC * (s16 ? 2 : 4)) : 0;
   const size_t o_ts = take((size_t)nqb * k * 4);
   const size_t o_ti = take((size_t)nqb * k * 8);
   const size_t o_th = take((size_t)nq * 4);   // every query's threshold (the overflow pass reuses them)
@@ -1948,12 +1956,13 @@ static int search_bounded(clm_index* x, bool sampled, int64_t S, const u16* q16,
     if (sampled) {
       GemmArgs ga{};
       ga.A = q16 + q0 * dim; ga.lda = dim; ga.W = x->samp; ga.ldw = dim;
-      ga.M = (int)nb; ga.N = (int)S; ga.K = dim; ga.out = sc; ga.ldo = ldS; ga.out16 = s16 ? 1 : 0;
+      ga.M = (int)nb; ga.N = (int)S; ga.K = dim; ga.out = sc; ga.ldo = ldC; ga.out16 = sgrp ? 2 : s16 ? 1 : 0;
       ga.rscale = qinv + q0; ga.cscale = x->samp_inv;
-      KCHK(gemm(false, EPI_SCORE, ga, st));
+      if (sgrp) KCHK(gemm_cfg(false, EPI_SCORE, 1, ga, st));   // config 1 (256 x 256): the group layout's tile
+      else KCHK(gemm(false, EPI_SCORE, ga, st));
       if (s16) {
-        KCHK(kth_thresholds16((const u16*)sc, ldS, nb, S, k, RESCORE_MARGIN, th + q0, st));
-        KCHK(count_ge16((const u16*)sc, ldS, nb, S, th + q0, est + q0, st));
+        KCHK(kth_thresholds16((const u16*)sc, ldC, nb, Sc, k, RESCORE_MARGIN, th + q0, st));
+        KCHK(count_ge16((const u16*)sc, ldC, nb, Sc, th + q0, est + q0, st));
       } else {
         if (k <= 8 && !g_kth_radix) {   // one streaming pass for the k-th value alone
           KCHK(kth_thresholds(sc, ldS, nb, S, k, RESCORE_MARGIN, th + q0, st));
@@ -1984,7 +1993,7 @@ static int search_bounded(clm_index* x, bool sampled, int64_t S, const u16* q16,
     bool dense = false;
     if (sampled) {
       int64_t over = 0;
-      for (int64_t i = 0; i < nb; ++i) over += (double)hest[q0 + i] * ((double)N / (double)S) > CAND_CAP;
+      for (int64_t i = 0; i < nb; ++i) over += (double)hest[q0 + i] * (sgrp ? 4.0 : 1.0) * ((double)N / (double)S) > CAND_CAP;
       dense = 2 * over > nb;
     }
     GemmArgs gf{};

@@ -288,6 +288,39 @@ __device__ __forceinline__ void epilogue(const GemmArgs& g, const f32x4 (&acc)[B
       if constexpr (EPI == EPI_FILTER) th[mb] = m < g.M ? g.theta[(int64_t)m * g.theta_ld] : 0.f;
     }
     if constexpr (EPI == EPI_SCORE) {
+      if constexpr (C::TN == 8) {
+        if (g.out16 == 2) {
+          // the largest of each lane's 4 consecutive scores, fp16 rounded toward -inf: a row's
+          // tile of BN columns becomes BN / 4 group maxima, lane (wn, q)'s 8 blocks contiguous at
+          // n0 / 4 + wn * (BN / WN) / 4 + q * 8 (a permutation of the groups: the k-th value and
+          // count passes read a row's values as a multiset). NaN-propagating maximum.
+          const auto oh = buf_rsrc((const u16*)g.out + out_off + (int64_t)m0 * g.ldo, nrec);
+          const int q = lane >> 4;
+          const int ccol = n0 / 4 + wn * (BN / WN) / 4 + q * 8;
+#pragma unroll
+          for (int mb = 0; mb < C::TM; ++mb) {
+            const int m = wrow + mb * 16;
+            uint32_t w[4];
+#pragma unroll
+            for (int nb = 0; nb < 8; nb += 2) {
+              float mx2[2];
+#pragma unroll
+              for (int u = 0; u < 2; ++u) {
+                const float4 c = cv[nb + u];
+                const f32x4 a = acc[mb][nb + u];
+                mx2[u] = __builtin_elementwise_maximum(
+                    __builtin_elementwise_maximum(a[0] * rs[mb] * c.x, a[1] * rs[mb] * c.y),
+                    __builtin_elementwise_maximum(a[2] * rs[mb] * c.z, a[3] * rs[mb] * c.w));
+              }
+              w[nb / 2] = f16_down(mx2[0]) | (f16_down(mx2[1]) << 16);
+            }
+            // every column of the lane's blocks is < N when its first one is (N % 256 == 0 here)
+            const uint32_t off = (m < g.M && wcol < g.N) ? (uint32_t)(((int64_t)(m - m0) * g.ldo + ccol) * 2) : BUF_OOB;
+            __builtin_amdgcn_raw_buffer_store_b128(u32x4{w[0], w[1], w[2], w[3]}, oh, off, 0, 0);
+          }
+          return;
+        }
+      }
       if (g.out16) {   // fp16 scores rounded toward -inf, 8 B per lane and block
         const auto oh = buf_rsrc((const u16*)g.out + out_off + (int64_t)m0 * g.ldo, nrec);
 #pragma unroll

@@ -39,7 +39,9 @@ struct GemmArgs {
   // into ksplit equal slices; slice s of every tile writes out + s * split_stride
   int ksplit; int64_t split_stride;
   // EPI_SCORE: 1 = store the scores as fp16 rounded toward -inf (f16_down: never above the fp32
-  // score, so a k-th largest taken over them bounds the fp32 one from below), out as u16 [M, ldo]
+  // score, so a k-th largest taken over them bounds the fp32 one from below), out as u16 [M, ldo];
+  // 2 (gemm_kernel config 1 only, N % 256 == 0) = one fp16 (rounded down) per 4 consecutive
+  // columns, their maximum, out as u16 [M, ldo >= N / 4] in a per-tile permuted column order
   int out16;
   // varlen rows (packed text tower): if set, the row count is *m_dev (device-resident, <= M, which
   // sizes the grid), so a captured graph replays with data-dependent row counts
