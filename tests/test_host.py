@@ -160,3 +160,41 @@ def test_gemm_config_table_matches_the_test_matrix():
     (test_gpu_kernels.py) covers exactly these ids"""
     from clip_lora_match_amd import _capi as C
     assert C.lib().clm_gemm_num_configs() == 13
+
+
+def _f16_down(v):
+    """numpy restatement of clm_common.hpp f16_down: the largest fp16 value <= v"""
+    import numpy as np
+    h = v.astype(np.float16)
+    b = h.view(np.uint16).astype(np.int32)
+    up = h.astype(np.float32) > v
+    b = np.where(up & (b == 0), 0x8001, np.where(up & (b >= 0x8000), b + 1, np.where(up, b - 1, b)))
+    return b.astype(np.uint16).view(np.float16)
+
+
+def test_sampled_threshold_stays_a_lower_bound():
+    """The bounded search's sampled θ (capi.cpp search_bounded) is the k-th largest of the stored
+    sample scores minus the margin; round 5 stores them as fp16 rounded toward -inf and as maxima
+    of groups of 4 sample rows. Both only lower the k-th largest: f16_down(v) <= v for every v
+    (ties, subnormals, signs, infinities), and the k-th largest of group maxima (a subset of the
+    values) is <= the k-th largest of all values -- so θ never rises above the fp32 one."""
+    import numpy as np
+    g = np.random.default_rng(5)
+    v = np.concatenate([g.normal(0, 0.05, 200000), g.uniform(-1, 1, 20000),
+                        np.float32(2.0) ** g.integers(-30, 5, 2000) * g.choice([-1, 1], 2000),
+                        [0.0, -0.0, 1.0, -1.0, 65504.0, 1e6, -1e6, np.inf, -np.inf, 6e-8, -6e-8]]).astype(np.float32)
+    with np.errstate(over="ignore"):
+        h = _f16_down(v)
+        rne = v.astype(np.float16)
+    assert (h.astype(np.float32) <= v).all()
+    fin = np.abs(v) <= 65504   # in range: RNE or the fp16 value one step below it
+    down_one = h.astype(np.float32) == np.nextafter(rne, np.float16(-np.inf)).astype(np.float32)
+    assert ((h == rne) | down_one)[fin].all()
+    for k in (1, 5, 8):
+        for _ in range(5):
+            s = g.normal(0.0, 0.044, 195328).astype(np.float32)     # one query's sample scores
+            kth32 = np.sort(s)[-k]
+            grp = _f16_down(s.reshape(-1, 4).max(1)).astype(np.float32)
+            kth_grp = np.sort(grp)[-k]
+            assert kth_grp <= kth32
+            assert kth32 - kth_grp < 0.05   # and it stays close (more candidates, not a collapse)
