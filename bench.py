@@ -94,6 +94,8 @@ def parse_args(argv=None):
                     help="encode batch of the configs[2] leg (1280: profiles/r04_v8_index_batch_sweep.txt)")
     ap.add_argument("--no-persist", action="store_true", help="skip the search index shard save / load timing")
     ap.add_argument("--no-near-dup", action="store_true", help="skip the near-duplicate-rows search leg")
+    ap.add_argument("--no-single", action="store_true", help="skip the one-query-per-call search leg")
+    ap.add_argument("--no-encode-item", action="store_true", help="skip the per-item encode_image / encode_text leg")
     ap.add_argument("--sequential", action="store_true", help="towers back to back on one stream, no graph")
     ap.add_argument("--split", type=int, default=0, help="sub-batches per tower in encode_pair (0 = library default)")
     ap.add_argument("--no-trace", action="store_true", help="skip the rocprofv3 kernel trace of the headline step")
@@ -302,8 +304,67 @@ def shard_roundtrip(idx, q, k) -> dict:
             "reloaded_search_identical": same, "where": "a temporary file (the box's /tmp)"}
 
 
+def single_query_leg(idx, q, chk_s, chk_i, k: int, calls: int = 64) -> dict:
+    """The reference's own search call pattern on the configs[4] index: ONE query per call through
+    the drop-in TextSearchIndex.search_with_embedding(q, 5) (search.py:93-99; SeekerService.search_items
+    calls it per request, seeker_service.py:183-186), with the CPU float32 query tensor the reference's
+    encode_* returns. The small batch takes the one-pass streaming search (capi.cpp search_small:
+    the fp16 index read once, scan16_kernel). HBM bound: the 10 M x 512 fp16 rows + fp32 inverse
+    norms per query. Also the device-level call (CosineIndex.search, device queries) and nq = 1..16
+    per call, and equality with the exact fp64 scan (scores and indices) on the check queries."""
+    from clip_lora_match_amd.search import TextSearchIndex
+    tsi = TextSearchIndex.from_gpu_index(idx)
+    n, dim = len(idx), idx.dim
+    nbytes = n * dim * 2 + n * 4
+    qs_cpu = q[:calls].float().cpu()
+    for j in range(3):
+        tsi.search_with_embedding(qs_cpu[j], k)
+    torch.cuda.synchronize()
+    st0 = idx.stats()
+    t0 = time.perf_counter()
+    res = [tsi.search_with_embedding(qs_cpu[j], k) for j in range(calls)]
+    t_call = (time.perf_counter() - t0) / calls
+    st1 = idx.stats()
+    nchk = min(chk_i.shape[0], calls)
+    ci, cs = chk_i.cpu(), chk_s.cpu()
+    eq = sum(1 for j in range(nchk) if [r.index for r in res[j]] == ci[j].tolist()
+             and [r.score for r in res[j]] == cs[j].tolist())
+    qd = q[:calls].contiguous()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for j in range(calls):
+        idx.search(qd[j:j + 1], k)
+    e1.record()
+    torch.cuda.synchronize()
+    t_dev = e0.elapsed_time(e1) * 1e-3 / calls
+    per_nq = {}
+    for nq in (1, 2, 4, 8, 16):
+        reps = 12
+        idx.search(qd[:nq], k)
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        for _ in range(reps):
+            idx.search(qd[:nq], k)
+        torch.cuda.synchronize()
+        dt = (time.perf_counter() - t1) / reps
+        per_nq[str(nq)] = {"ms_per_call": round(dt * 1e3, 3), "qps": round(nq / dt, 1),
+                           "hbm_frac": round(nbytes / dt / (HBM_PEAK_GBS * 1e9), 4)}
+    served = {key: st1[key] - st0[key] for key in st1}
+    return {"ms_per_query": round(t_call * 1e3, 3), "qps": round(1.0 / t_call, 1),
+            "hbm_bytes_per_query": nbytes,
+            "hbm_frac": round(nbytes / t_call / (HBM_PEAK_GBS * 1e9), 4),
+            "device_ms_per_query": round(t_dev * 1e3, 3),
+            "device_hbm_frac": round(nbytes / t_dev / (HBM_PEAK_GBS * 1e9), 4),
+            "calls": calls, "k": k, "rows": n,
+            "equal_to_exact_scan": f"{eq}/{nchk}",
+            "paths": served, "per_call_batch": per_nq,
+            "api": "TextSearchIndex.search_with_embedding(q, 5), q a CPU float32 (512,) tensor, results as "
+                   "SearchResult lists; device_*: CosineIndex.search on a device query, HIP events",
+            "hbm_frac_def": "(N x 512 x 2 B fp16 rows + N x 4 B inverse norms) / time per query / 8 TB/s"}
+
+
 def search_leg(rows: int, queries: int, k: int, device, world: int = 1, rank: int = 0, keep_host: bool = False,
-               persist_shard: bool = False):
+               persist_shard: bool = False, single: bool = False):
     """BASELINE configs[4]: 10k fp16 query embeddings vs a rows x 512 fp16 index in HBM, top-k
     by exact cosine (fp16 MFMA pass + exact re-score of the candidates).
     world > 1: the index is row-sharded (rank r holds shard_range(rows, r, world)
@@ -392,12 +453,18 @@ def search_leg(rows: int, queries: int, k: int, device, world: int = 1, rank: in
     persist = None
     if persist_shard and world == 1:
         persist = shard_roundtrip(idx, q[:256], k)
-    idx.close()
     # the check subset: gather every rank's exact top-k, order the union, compare with the fast path
     if world > 1:
         from clip_lora_match_amd.distributed import gather_candidates
         chk_s, chk_i = gather_candidates(chk_s.contiguous(), chk_i.contiguous())
     chk_s, chk_i = _topk_ordered(chk_s, chk_i, k)
+    single_res = None
+    if single and world == 1:
+        try:
+            single_res = single_query_leg(idx, q, chk_s, chk_i, k)
+        except Exception as e:   # reported, never hidden
+            single_res = {"error": repr(e)}
+    idx.close()
     match = int((torch.eq(chk_i, i[:nchk]).all(1) & torch.eq(chk_s, s[:nchk]).all(1)).sum())
     import hashlib
     flops = 2.0 * queries * rows * dim
@@ -412,6 +479,8 @@ def search_leg(rows: int, queries: int, k: int, device, world: int = 1, rank: in
            "topk_sha256": hashlib.sha256(i.cpu().numpy().tobytes()).hexdigest()[:16]}
     if persist is not None:
         out["persist"] = persist
+    if single_res is not None:
+        out["single"] = single_res
     if world > 1:
         out.update({"n_gpus": world, "shard_rows": stop - start,
                     "parallelism": "row-sharded index, replicated queries, all_gather(top-k) + GPU merge"})
@@ -464,6 +533,72 @@ def near_dup_search_leg(device, rows: int = 1_000_000, groups: int = 64, group_r
             "tie_groups": groups, "group_rows": group_rows,
             "paths_timed_block": {key: after[key] - before.get(key, 0) for key in after},
             "equal_to_full_exact_scan": bool(torch.equal(i, i_ref) and torch.equal(s, s_ref))}
+
+
+def encode_item_leg(device, dtype: str, calls: int = 32) -> dict:
+    """The reference's per-item API (models/clip_model.py:89-150; embed_image / embed_text call it per
+    item): encode_image(path) on a 640 x 480 JPEG (host decode with PIL, GPU bicubic resize + centre
+    crop, batch-1 encode, CPU float32 result) and encode_text(str) (host BPE tokenizer -- the committed
+    fixture vocabulary, no CLIP vocab ships here -- batch-1 encode), through load_clip_model with the
+    synthetic B/32 weights and LoRA r=8 on q,k,v,out. Also the GPU encode alone at batch 1 on resident
+    pixels / ids, so the host share (decode, tokenize, copies) is visible."""
+    import shutil
+    import tempfile
+    import yaml
+    from PIL import Image
+    from clip_lora_match_amd.clip_model import encode_image, encode_text, load_clip_model
+    d = tempfile.mkdtemp(prefix="clm_item_")
+    try:
+        cfgp = os.path.join(d, "clip_config.yaml")
+        with open(cfgp, "w") as f:
+            yaml.safe_dump({"model": {"name": "openai/clip-vit-base-patch32", "device": "cuda",
+                                      "tokenizer_dir": os.path.join(REPO, "tests", "golden", "clip_bpe")},
+                            "preprocess": {"image_size": 224}}, f)
+        model, proc, dv = load_clip_model(cfgp, use_lora=True, lora_weights_path="synthetic",
+                                          weights_dir="synthetic", max_batch=1, compute_dtype=dtype)
+        paths = []
+        for i in range(4):
+            p = os.path.join(d, f"item{i}.jpg")
+            Image.fromarray(syn.images_u8(1, 480, 300 + i)[0]).resize((640, 480)).save(p, quality=90)
+            paths.append(p)
+        caps = ["a black leather wallet with a student card", "blue umbrella left near the library entrance",
+                "dompet hitam ditemukan di kantin", "silver laptop charger with a frayed cable"]
+        for j in range(4):
+            encode_image(paths[j], model, proc, dv)
+            encode_text(caps[j], model, proc, dv)
+        t0 = time.perf_counter()
+        for j in range(calls):
+            encode_image(paths[j % 4], model, proc, dv)
+        t1 = time.perf_counter()
+        for j in range(calls):
+            encode_text(caps[j % 4], model, proc, dv)
+        t2 = time.perf_counter()
+        px = proc.images_u8([paths[0]], dv)
+        ids = proc.token_ids([caps[0]]).to(dv)
+        for _ in range(3):
+            model.encode_pixels(px)
+            model.encode_ids(ids)
+        torch.cuda.synchronize()
+        t3 = time.perf_counter()
+        for _ in range(calls):
+            model.encode_pixels(px)
+            torch.cuda.synchronize()
+        t4 = time.perf_counter()
+        for _ in range(calls):
+            model.encode_ids(ids)
+            torch.cuda.synchronize()
+        t5 = time.perf_counter()
+        model.close()
+    finally:
+        shutil.rmtree(d, ignore_errors=True)
+    ms = lambda a, b: round((b - a) / calls * 1e3, 3)   # noqa: E731
+    return {"encode_image_ms": ms(t0, t1), "encode_text_ms": ms(t1, t2),
+            "gpu_encode_image_ms": ms(t3, t4), "gpu_encode_text_ms": ms(t4, t5),
+            "images_per_s": round(calls / (t1 - t0), 1), "texts_per_s": round(calls / (t2 - t1), 1),
+            "calls": calls, "dtype": DTYPE_LABEL.get(dtype, dtype), "text_tokens": int(ids.shape[1]),
+            "api": "clip_model.encode_image(path) / encode_text(str), one item per call (CPU float32 out); "
+                   "gpu_*: ClipLoraModel.encode_pixels / encode_ids at batch 1 on resident inputs, synchronised",
+            "image": "640 x 480 JPEG (quality 90), shortest-edge 224 bicubic + centre crop on the GPU"}
 
 
 def l14_leg(device, batch: int = 128, steps: int = 3, warmup: int = 1, dtype: str = "float16"):
@@ -787,8 +922,9 @@ def parity_vs_golden(model, cfg, dev) -> dict:
 
 def lora_unmerged_leg(cfg, sd, lora, dev, B, imgs, ids, steps, warmup, dtype):
     """The same step with the LoRA adapters kept unmerged (hot-swappable, models/clip_model.py:65-79):
-    the K-extension mode, Y = [X | X A^T] . [W | (alpha/r) B]^T, A's down-projection computed in the
-    LayerNorm kernel (q/k/v, fc1 inputs) or by lora_down (out_proj, fc2 inputs)."""
+    the K-extension mode, Y = [X | X A^T] . [W | (alpha/r) B]^T, the down-projection X A^T written into
+    the activation's extension columns by a skinny MFMA GEMM (64 x 64 tiles, GEMM config 12) per LoRA'd
+    input (q/k/v after LN1, out_proj after attention; capi.cpp lora_down_gemm)."""
     m = ClipLoraModel(cfg, device=dev, compute_dtype=dtype, lora_mode="unmerged", max_batch=B)
     m.load_tensors(sd)
     m.load_tensors(lora)
@@ -1114,7 +1250,8 @@ def main():
     if not args.no_search:   # every rank takes part when the index is sharded (world > 1)
         keep = rank == 0 and world == 1 and not args.no_cpu_baseline
         sr, host16, qs_host, gpu_i = search_leg(args.search_rows, args.search_queries, 5, dev, world, rank,
-                                                keep_host=keep, persist_shard=not args.no_persist)
+                                                keep_host=keep, persist_shard=not args.no_persist,
+                                                single=not args.no_single)
         if rank == 0:
             result["search"] = sr
     if rank == 0 and world == 1 and not args.no_search and not args.no_near_dup:
@@ -1122,6 +1259,11 @@ def main():
             result["search_near_dup"] = near_dup_search_leg(dev)
         except Exception as e:  # report, never hide
             result["search_near_dup"] = {"error": repr(e)}
+    if rank == 0 and world == 1 and not args.no_encode_item:
+        try:
+            result["encode_item"] = encode_item_leg(dev, args.dtype)
+        except Exception as e:  # report, never hide
+            result["encode_item"] = {"error": repr(e)}
     if rank == 0 and world == 1 and not args.no_l14:
         try:
             result["l14"] = l14_leg(dev, dtype=args.dtype)
@@ -1136,6 +1278,12 @@ def main():
                         f"{enc['threads']} threads; per-item (the reference's encode_image/encode_text pattern): "
                         f"{enc['per_item']['pairs_per_s']} pairs/s over {enc['per_item']['calls']} calls",
               "encode": enc}
+        if isinstance(result.get("encode_item"), dict) and "error" not in result["encode_item"]:
+            result["encode_item"]["cpu_reference_per_item_ms"] = {
+                "encode_image": round(1e3 / enc["per_item"]["images_per_s"], 2),
+                "encode_text": round(1e3 / enc["per_item"]["texts_per_s"], 2),
+                "note": "cpu_baseline.encode.per_item: transformers CLIPModel fp32 + LoRA hooks, batch 1, on "
+                        "preprocessed pixel_values / token ids (no decode or tokenizer)"}
         if host16 is not None:
             cb["search"] = cpu_search_baseline(host16, qs_host, 5, args.cpu_search_queries, args.cpu_search_budget,
                                                gpu_i)

@@ -16,7 +16,7 @@ LIB_PATH = os.environ.get("CLM_LIB", os.path.join(_HERE, "libclm.so"))
 
 CLM_OK, CLM_E_ARG, CLM_E_OOM, CLM_E_HIP, CLM_E_STATE, CLM_E_MISSING = 0, -1, -2, -3, -4, -5
 CLM_F32, CLM_F16, CLM_BF16, CLM_U8, CLM_I32, CLM_I64 = 0, 1, 2, 3, 4, 5
-CLM_ATTN_CAUSAL, CLM_ATTN_Q_LOG2E = 1, 2   # clm_attention flags
+CLM_ATTN_CAUSAL, CLM_ATTN_Q_LOG2E = 1, 2   # clm_attention_ex flags
 CLM_PIX_U8_HWC, CLM_PIX_F32_CHW = 0, 1
 CLM_LORA_MERGED, CLM_LORA_UNMERGED = 0, 1
 CLM_COMPUTE_MIXED = 0x12   # bf16 vision tower, fp16 text tower (clm.h)
@@ -106,6 +106,9 @@ def lib():
         "clm_gemm_num_configs": (c_int, []),
         "clm_debug_set": (None, [c_int]),
         "clm_attention": (c_int, [c_int, c_int, c_int, c_void_p, c_void_p, c_int64, c_int, c_int, c_int, c_void_p]),
+        "clm_gemm_scores16": (c_int, [c_int, c_int, c_void_p, c_int64, c_void_p, c_int64, c_int, c_int, c_int,
+                                      c_void_p, c_void_p, c_void_p, c_int64, c_int, c_void_p]),
+        "clm_attention_ex": (c_int, [c_int, c_int, c_int, c_void_p, c_void_p, c_int64, c_int, c_int, c_int, c_void_p]),
         "clm_layernorm": (c_int, [c_int, c_int, c_void_p, c_int64, c_int64, c_int, c_void_p, c_void_p, c_float, c_void_p,
                                   c_int64, c_void_p]),
         "clm_prof_read": (c_int, [c_void_p, c_int, POINTER(ctypes.c_double), POINTER(ctypes.c_double),
@@ -127,7 +130,7 @@ EXPORTED = (
     "clm_cosine_scores", "clm_topk_merge", "clm_topk_threshold", "clm_l2_normalize", "clm_fuse_queries", "clm_resize_crop", "clm_synth_images", "clm_index_has_f32", "clm_index_export", "clm_index_import",
     "clm_last_error", "clm_version",
     "clm_model_desc_size", "clm_prof_enable", "clm_prof_read", "clm_gemm", "clm_gemm_num_configs",
-    "clm_attention", "clm_layernorm", "clm_debug_set",
+    "clm_attention", "clm_attention_ex", "clm_gemm_scores16", "clm_layernorm", "clm_debug_set",
 )
 CLM_EPI_STORE, CLM_EPI_GELU, CLM_EPI_RESID, CLM_EPI_SCORE = 0, 1, 2, 4
 CLM_PROF_GEMM, CLM_PROF_ATTN, CLM_PROF_LN, CLM_PROF_OTHER = 0, 1, 2, 3

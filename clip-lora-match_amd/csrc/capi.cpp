@@ -168,7 +168,7 @@ struct clm_ctx {
   hipEvent_t ev_fork = nullptr, ev_done = nullptr;
   typedef std::tuple<const void*, int, int, const void*, int, int, void*, void*, int, int, int> PairKey;
   std::map<PairKey, hipGraphExec_t> graphs;
-  int last_pair_path = -1;   // clm_pair_path: 0 = two tower streams, 1 = grouped launches
+  int last_pair_path = -1;   // clm_pair_path: 0 = two tower streams (-1: no encode_pair yet)
   // kernel timing (clm_prof_*): events recorded on the launch stream
   bool prof = false;
   std::vector<hipEvent_t> ev_pool;
@@ -235,7 +235,8 @@ struct clm_index {
   // queries served by: [0] sampled bounded search, [1] the full exact scan, [2] overflow re-runs,
   // [3] bounded search with the chunked fp16 scan as step 1
   // [4] / [5]: queries whose filter pass ran on G2 256 x 192 / gemm_kernel 256 x 256 (dense blocks)
-  int64_t search_stats[6] = {0, 0, 0, 0, 0, 0};
+  // [6]: queries served by the small-batch streaming search (search_small)
+  int64_t search_stats[7] = {0, 0, 0, 0, 0, 0, 0};
 };
 
 namespace {
@@ -597,7 +598,7 @@ bool fused_attention(int T, int H, int d, int K) {
   return v == 1 && !(g_gemm_debug & 16) && gemm_attn_supported(T, H, d, K);
 }
 
-// Per-call state of one tower's encoder pass (run_layers / run_layers_pair).
+// Per-call state of one tower's encoder pass (run_layers).
 struct LayerRun {
   Tower* T;
   int B, S;
@@ -623,15 +624,6 @@ int make_run(clm_ctx* c, Tower& T, int B, int S, bool causal, const int32_t* ids
   return CLM_OK;
 }
 
-// layer l's fused q/k/v + attention problem of one tower (gemm_attn / gemm_attn_varlen arguments)
-AttnProblem attn_problem(const LayerRun& R, int l) {
-  Tower& T = *R.T;
-  const LayerW& Lw = T.layers[l];
-  AttnProblem p{T.X, T.ldx, Lw.w_qkv, Lw.k_qkv, Lw.b_qkv, T.O, T.ldo, R.B, R.S, T.H, T.d, Lw.kl_qkv,
-                nullptr, nullptr, nullptr, nullptr};
-  if (R.vl) { p.lens = T.vl_lens; p.offs = T.vl_offs; p.tiles = T.vl_tiles; p.counts = T.vl_counts; }
-  return p;
-}
 double attn_flops(const LayerRun& R, int l) {
   const Tower& T = *R.T;
   return 2.0 * R.Mx * 3 * T.d * T.layers[l].kl_qkv + 4.0 * T.H * R.attn_pairs * 64;
@@ -780,74 +772,6 @@ int run_layers(clm_ctx* c, Tower& T, int B, int S, bool causal, const int32_t* i
   return r;
 }
 
-// Grouped mode of clm_encode_pair ($CLM_PAIR_GROUPED=1 or clm_debug_set bit 64; default off): the image and text towers'
-// layer l run as ONE launch per op on one stream -- fused q/k/v + attention (gemm_attn_pair),
-// out_proj and fc2 (gemm_pair RESID), LN2 / LN1 (layernorm_pair), fc1 (gemm_pair GELU) -- so the
-// two towers' tiles share the launches' rounds instead of two persistent kernels taking the chip
-// in turn (tile counts per launch: 400 + 462 RESID tiles over 512 slots, etc.). Every output bit
-// equals the two-stream path's (the pair kernels run each tower's tiles with that tower's code).
-// Layers 0 .. L-2 and the last layer's attention are grouped; the last layer's pruned row-wise
-// tail runs per tower (pair_launch puts each on its own stream).
-// Measured (round 5, B/32 batch 256, mixed): bit-identical, the pair kernels' summed time per step
-// 0.29 ms BELOW the two-stream step's kernels (the 160 x 128 RESID tiles pay once nothing else
-// wants the slots), but the step is 5.54 vs 4.92 ms: on two streams one tower's LayerNorms and
-// launch tails run under the other tower's GEMMs (~0.7 ms of kernel time hidden per step), which
-// one grouped chain cannot do (profiles/r05_v1_grouped_pair_ab.txt, r05_v1_grouped_pair_timeline.txt).
-bool pair_grouped() {
-  static int v = -1;
-  if (v < 0) {
-    const char* e = getenv("CLM_PAIR_GROUPED");
-    v = (e && atoi(e)) ? 1 : 0;
-  }
-  return v == 1 || (g_gemm_debug & 64);
-}
-int pair_persist() {   // $CLM_PAIR_PERSIST=1: persistent ranges instead of one tile per workgroup
-  static const int v = getenv("CLM_PAIR_PERSIST") ? atoi(getenv("CLM_PAIR_PERSIST")) : 0;
-  return v;
-}
-
-int run_layers_pair(clm_ctx* c, const LayerRun& V, const LayerRun& X, hipStream_t st) {
-  Tower& TV = *V.T;
-  Tower& TX = *X.T;
-  const int L = TV.L;
-  const bool fused = fused_attention(V.S, TV.H, TV.d, TV.layers[0].k_qkv) &&
-                     (X.vl || fused_attention(X.S, TX.H, TX.d, TX.layers[0].k_qkv));
-  for (int l = 0; l < L; ++l) {
-    if (fused) {
-      PROF(CLM_PROF_GEMM, attn_flops(V, l) + attn_flops(X, l));
-      KCHK(gemm_attn_pair(V.bf, X.bf, attn_problem(V, l), attn_problem(X, l), st));
-    } else {
-      int r = attn_step(c, V, l, st);
-      if (!r) r = attn_step(c, X, l, st);
-      if (r) return r;
-    }
-    if (l + 1 == L) break;   // the last layer's tail: per tower (pooled rows)
-    PostOps pv = post_ops(c, V, l, (int64_t)V.B * V.S, TV.h, TV.O, false);
-    PostOps px = post_ops(c, X, l, (int64_t)X.B * X.S, TX.h, TX.O, false);
-    const LayerW &Lv = TV.layers[l], &Lx = TX.layers[l];
-    if (Lv.r_out) KCHK(lora_down_gemm(V.bf, TV.O, TV.ldo, pv.out.M, TV.d, Lv.a_out, V.mdev, st));
-    if (Lx.r_out) KCHK(lora_down_gemm(X.bf, TX.O, TX.ldo, px.out.M, TX.d, Lx.a_out, X.mdev, st));
-    { PROF(CLM_PROF_GEMM, 2.0 * (pv.rows * pv.out.N * pv.out.K + px.rows * px.out.N * px.out.K));
-      KCHK(gemm_pair(V.bf, X.bf, EPI_RESID, -1, pv.out, px.out, pair_persist(), st)); }
-    { PROF(CLM_PROF_LN, (pv.rows * TV.d + px.rows * TX.d) * 6.0);
-      KCHK(layernorm_pair(V.bf, X.bf, pv.ln2, px.ln2, st)); }
-    if (Lv.r_fc1) KCHK(lora_down_gemm(V.bf, TV.X, TV.ldx, pv.fc1.M, TV.d, Lv.a_fc1, V.mdev, st));
-    if (Lx.r_fc1) KCHK(lora_down_gemm(X.bf, TX.X, TX.ldx, px.fc1.M, TX.d, Lx.a_fc1, X.mdev, st));
-    { PROF(CLM_PROF_GEMM, 2.0 * (pv.rows * pv.fc1.N * pv.fc1.K + px.rows * px.fc1.N * px.fc1.K));
-      KCHK(gemm_pair(V.bf, X.bf, EPI_GELU, -1, pv.fc1, px.fc1, pair_persist(), st)); }
-    if (Lv.r_fc2) KCHK(lora_down_gemm(V.bf, TV.Hm, TV.ldm, pv.fc2.M, TV.mlp, Lv.a_fc2, V.mdev, st));
-    if (Lx.r_fc2) KCHK(lora_down_gemm(X.bf, TX.Hm, TX.ldm, px.fc2.M, TX.mlp, Lx.a_fc2, X.mdev, st));
-    { PROF(CLM_PROF_GEMM, 2.0 * (pv.rows * pv.fc2.N * pv.fc2.K + px.rows * px.fc2.N * px.fc2.K));
-      KCHK(gemm_pair(V.bf, X.bf, EPI_RESID, -1, pv.fc2, px.fc2, pair_persist(), st)); }
-    { PROF(CLM_PROF_LN, (pv.rows * TV.d + px.rows * TX.d) * 6.0);
-      KCHK(layernorm_pair(V.bf, X.bf, pv.ln1, px.ln1, st)); }
-    const LayerW &Nv = TV.layers[l + 1], &Nx = TX.layers[l + 1];
-    if (Nv.r_qkv) KCHK(lora_down_gemm(V.bf, TV.X, TV.ldx, pv.fc1.M, TV.d, Nv.a_qkv, V.mdev, st));
-    if (Nx.r_qkv) KCHK(lora_down_gemm(X.bf, TX.X, TX.ldx, px.fc1.M, TX.d, Nx.a_qkv, X.mdev, st));
-  }
-  return CLM_OK;
-}
-
 // the tower with its workspace pointers moved to sub-batch b0 (items of `rows` sequence rows)
 Tower ws_view(const Tower& T0, int b0, int rows, int patches, int proj_dim) {
   Tower T = T0;
@@ -990,21 +914,49 @@ int clm_gemm(int hip_device, int dtype, int epilogue, int config, const void* A,
 
 int clm_gemm_num_configs(void) { return gemm_num_configs(); }
 
+// The sampled search's score matrix forms (search_bounded): fp16 A / W, score = acc * rscale[m] *
+// cscale[n] stored as fp16 rounded toward -inf (mode 1, [M, ldo] u16) or as the maxima of each
+// group of 4 consecutive columns, rounded the same way (mode 2: [M, ldo >= N / 4] u16, a row's
+// groups in a fixed permutation; config 1 and N % 256 == 0, as the search runs it).
+int clm_gemm_scores16(int hip_device, int config, const void* A, int64_t lda, const void* W, int64_t ldw, int M,
+                      int N, int K, const float* rscale, const float* cscale, void* out, int64_t ldo, int mode,
+                      void* stream) {
+  if (mode != 1 && mode != 2) return fail(CLM_E_ARG, "mode must be 1 (fp16 scores) or 2 (group maxima)");
+  if (config >= gemm_num_configs()) return fail(CLM_E_ARG, "bad config");
+  if (M < 0 || N < 0 || K <= 0 || K % 64) return fail(CLM_E_ARG, "bad shape (K % 64 == 0)");
+  if (mode == 2 && (config != 1 || N % 256 || ldo < N / 4 || ldo % 8))
+    return fail(CLM_E_ARG, "group maxima: config 1, N % 256 == 0, ldo >= N / 4, ldo % 8 == 0");
+  if (mode == 1 && ldo < N) return fail(CLM_E_ARG, "ldo < N");
+  DeviceGuard g(hip_device);
+  GemmArgs a{};
+  a.A = (const u16*)A; a.lda = lda; a.W = (const u16*)W; a.ldw = ldw; a.M = M; a.N = N; a.K = K;
+  a.out = out; a.ldo = ldo; a.rscale = rscale; a.cscale = cscale; a.out16 = mode;
+  hipError_t e = gemm_cfg(false, EPI_SCORE, config, a, (hipStream_t)stream);
+  if (e != hipSuccess) return fail(CLM_E_HIP, std::string("gemm: ") + hipGetErrorString(e));
+  return CLM_OK;
+}
+
 void clm_debug_set(int flags) { g_gemm_debug = flags; }
 
-int clm_attention(int hip_device, int dtype, int causal, const void* qkv, void* out, int64_t ldo, int B, int T,
-                  int H, void* stream) {
+int clm_attention_ex(int hip_device, int dtype, int flags, const void* qkv, void* out, int64_t ldo, int B, int T,
+                     int H, void* stream) {
   if (dtype != CLM_BF16 && dtype != CLM_F16) return fail(CLM_E_ARG, "dtype must be bf16 or f16");
   if (B < 0 || T < 0 || H <= 0) return fail(CLM_E_ARG, "bad shape");
   DeviceGuard g(hip_device);
-  if (causal & ~(CLM_ATTN_CAUSAL | CLM_ATTN_Q_LOG2E)) return fail(CLM_E_ARG, "unknown attention flags");
-  const bool bf = dtype == CLM_BF16, cz = (causal & CLM_ATTN_CAUSAL) != 0, l2e = (causal & CLM_ATTN_Q_LOG2E) != 0;
+  if (flags & ~(CLM_ATTN_CAUSAL | CLM_ATTN_Q_LOG2E)) return fail(CLM_E_ARG, "unknown attention flags");
+  const bool bf = dtype == CLM_BF16, cz = (flags & CLM_ATTN_CAUSAL) != 0, l2e = (flags & CLM_ATTN_Q_LOG2E) != 0;
   if (l2e && !attention_folds_log2e(bf, cz, T))
     return fail(CLM_E_ARG, "CLM_ATTN_Q_LOG2E: the kernel for this dtype / mask / T takes q without log2(e)");
   hipError_t e = attention(bf, cz, (const u16*)qkv, 3LL * H * 64, (u16*)out, ldo, B, T, H, H * 64,
                            (hipStream_t)stream, l2e);
   if (e != hipSuccess) return fail(CLM_E_HIP, std::string("attention: ") + hipGetErrorString(e));
   return CLM_OK;
+}
+
+// the original entry point: `causal` is a 0 / non-0 switch (any non-zero value is the causal mask)
+int clm_attention(int hip_device, int dtype, int causal, const void* qkv, void* out, int64_t ldo, int B, int T,
+                  int H, void* stream) {
+  return clm_attention_ex(hip_device, dtype, causal ? CLM_ATTN_CAUSAL : 0, qkv, out, ldo, B, T, H, stream);
 }
 
 int clm_layernorm(int hip_device, int dtype, const float* src, int64_t lds, int64_t M, int d, const float* gamma,
@@ -1236,12 +1188,6 @@ int clm_encode_text(clm_ctx* ctx, const int32_t* ids, int n, int L, void* out, i
 // Sub-batch launches of one encode_pair on ps[0..2*split): images on ps[2j], captions on
 // ps[2j+1]. `fork` has been recorded on ps[0]; every other stream waits on it, and ps[0]
 // waits on every other stream's pev at the end (join).
-// whether clm_encode_pair runs the grouped layers (run_layers_pair) for these arguments
-static bool pair_uses_grouped(const clm_ctx* c, int split, int n_img, int n_txt) {
-  return split == 1 && n_img > 0 && n_txt > 0 && pair_grouped() && c->vis.L == c->txt.L && c->vis.L > 0 &&
-         c->bf16(true) >= c->bf16(false);
-}
-
 static int pair_launch(clm_ctx* c, int split, hipEvent_t fork, const void* pixels, int layout, int n_img,
                        const int32_t* ids, int n_txt, int L, void* oi, void* ot, int out_dtype, int normalize) {
   const clm_model_desc& d = c->desc;
@@ -1254,33 +1200,6 @@ static int pair_launch(clm_ctx* c, int split, hipEvent_t fork, const void* pixel
     ~Concurrent() { gemm_set_concurrent(false); }
   } conc(n_img > 0 && n_txt > 0);
   const int G = d.image_size / d.patch;
-  if (pair_uses_grouped(c, split, n_img, n_txt)) {
-    // grouped: the two prologues on their own streams, then every layer's ops as one launch per
-    // op on ps[0], then each tower's pruned last-layer tail + pooling on its own stream again
-    Tower& V = c->vis;
-    Tower& X = c->txt;
-    hipStream_t sv = c->ps[0], sx = c->ps[1];
-    bool vl = false;
-    int r = image_prologue(c, V, pixels, layout, n_img, sv);
-    if (!r) r = text_prologue(c, X, ids, n_txt, L, &vl, sx);
-    if (r) return r;
-    HIPCHK(hipEventRecord(c->pev[1], sx));
-    HIPCHK(hipStreamWaitEvent(sv, c->pev[1], 0));
-    LayerRun RV, RX;
-    if ((r = make_run(c, V, n_img, G * G + 1, false, nullptr, false, sv, &RV))) return r;
-    if ((r = make_run(c, X, n_txt, L, true, ids, vl, sv, &RX))) return r;
-    if ((r = run_layers_pair(c, RV, RX, sv))) return r;
-    HIPCHK(hipEventRecord(c->pev[0], sv));
-    HIPCHK(hipStreamWaitEvent(sx, c->pev[0], 0));
-    bool pv = false, px = false;
-    if ((r = post_attn_step(c, RV, V.L - 1, &pv, sv))) return r;
-    if ((r = image_epilogue(c, V, n_img, pv, oi, out_dtype, normalize, sv))) return r;
-    if ((r = post_attn_step(c, RX, X.L - 1, &px, sx))) return r;
-    if ((r = text_epilogue(c, X, ids, n_txt, L, vl, px, ot, out_dtype, normalize, sx))) return r;
-    HIPCHK(hipEventRecord(c->pev[1], sx));
-    HIPCHK(hipStreamWaitEvent(c->ps[0], c->pev[1], 0));
-    return CLM_OK;
-  }
   for (int j = 0; j < split; ++j) {
     const int i0 = (int)((int64_t)n_img * j / split), i1 = (int)((int64_t)n_img * (j + 1) / split);
     const int t0 = (int)((int64_t)n_txt * j / split), t1 = (int)((int64_t)n_txt * (j + 1) / split);
@@ -1338,7 +1257,7 @@ int clm_encode_pair(clm_ctx* ctx, const void* pixels, int pix_layout, int n_img,
   if (!split) split = env_split > 0 ? env_split : 1;
   split = std::max(1, std::min({split, clm_ctx::MAX_SPLIT, std::max(n_img, n_txt)}));
   const bool use_graph = (flags & CLM_PAIR_GRAPH) && !ctx->prof;
-  ctx->last_pair_path = pair_uses_grouped(ctx, split, n_img, n_txt) ? 1 : 0;
+  ctx->last_pair_path = 0;   // one stream per tower piece (the only path; round 5's grouped launches were removed)
   HIPCHK(hipEventRecord(ctx->ev_fork, st));
   HIPCHK(hipStreamWaitEvent(ctx->ps[0], ctx->ev_fork, 0));
   if (!use_graph) {
@@ -1848,6 +1767,58 @@ static int overflow_wide(clm_index* x, const std::vector<int64_t>& qs, const std
   return CLM_OK;
 }
 
+// Candidate lists that overflowed CAND_CAP (queries `overflow`, first-pass counts `ocount`): rebuilt
+// whole by a second filter pass (overflow_wide) or redone by the exact scan (search_bounded,
+// search_small). th: every query's filter threshold.
+static int finish_overflow(clm_index* x, const std::vector<int64_t>& overflow, const std::vector<int64_t>& ocount,
+                           const u16* q16, const float* qinv, const float* q32, const double* qn, const float* th,
+                           int k, float* osc, int64_t* oix, hipStream_t st) {
+  const int dim = (int)x->dim;
+  int r;
+  // Candidate lists beyond CAND_CAP (near-duplicate rows inside the window). Lists of up to
+  // (SORT_MAX / k) chunks are rebuilt whole by a second filter pass over just those queries and
+  // re-scored chunk-wise (overflow_wide); longer ones are redone by the exact scan, all of them in
+  // ONE scan (the index is streamed once per query block of search_scan, not once per query).
+  x->search_stats[2] += (int64_t)overflow.size();
+  std::vector<int64_t> wide, wcount, full;
+  for (size_t j = 0; j < overflow.size(); ++j) {
+    // headroom over the first pass's count: a different tile shape may round a score differently
+    const int64_t cap2 = ocount[j] + ocount[j] / 8 + 256;
+    if ((cap2 + RESCORE_WIDE_CHUNK - 1) / RESCORE_WIDE_CHUNK * k <= 8192) {
+      wide.push_back(overflow[j]);
+      wcount.push_back(cap2);
+    } else {
+      full.push_back(overflow[j]);
+    }
+  }
+  if (!wide.empty() && (r = overflow_wide(x, wide, wcount, q16, qinv, q32, qn, th, k, osc, oix, full, st))) return r;
+  if (full.empty()) return CLM_OK;
+  const int64_t no = (int64_t)full.size();
+  size_t o2 = 0;
+  auto take2 = [&](size_t bytes) { size_t o = o2; o2 = round_up(o2 + bytes, 256); return o; };
+  const size_t p_x = take2((size_t)no * 8), p_q = take2((size_t)no * dim * 4), p_n = take2((size_t)no * 8),
+               p_s = take2((size_t)no * k * 4), p_i = take2((size_t)no * k * 8);
+  if ((r = grow(&x->ws4, &x->ws4_bytes, o2))) return r;   // overflow_wide is done with it (it drains its stream)
+  uint8_t* wo = (uint8_t*)x->ws4;
+  int64_t* gx = (int64_t*)(wo + p_x);
+  float* gq = (float*)(wo + p_q);
+  double* gn = (double*)(wo + p_n);
+  float* gs = (float*)(wo + p_s);
+  int64_t* gi = (int64_t*)(wo + p_i);
+  hipError_t e = hipMemcpyAsync(gx, full.data(), (size_t)no * 8, hipMemcpyHostToDevice, st);
+  if (e == hipSuccess) e = gather_rows(q32, (int64_t)dim * 4, gx, no, (int64_t)dim * 4, gq, (int64_t)dim * 4, false, st);
+  if (e == hipSuccess) e = gather_rows(qn, 8, gx, no, 8, gn, 8, false, st);
+  r = e == hipSuccess ? search_scan(x, true, nullptr, nullptr, gq, gn, no, k, gs, gi, st)
+                      : fail(CLM_E_HIP, std::string("overflow gather: ") + hipGetErrorString(e));
+  if (r == CLM_OK) e = gather_rows(gs, (int64_t)k * 4, gx, no, (int64_t)k * 4, osc, (int64_t)k * 4, true, st);
+  if (r == CLM_OK && e == hipSuccess) e = gather_rows(gi, (int64_t)k * 8, gx, no, (int64_t)k * 8, oix, (int64_t)k * 8, true, st);
+  (void)hipStreamSynchronize(st);
+  if (r) return r;
+  if (e != hipSuccess) return fail(CLM_E_HIP, std::string("overflow scatter: ") + hipGetErrorString(e));
+  return CLM_OK;
+}
+
+
 // Bounded search (large N), per block of queries:
 //  1. theta[q] <= the fp16-pass k-th best score of q:
 //     sampled (k <= 256, N >= 4S): the k-th best over a strided sample of S rows -- a subset
@@ -2025,47 +1996,79 @@ static int search_bounded(clm_index* x, bool sampled, int64_t S, const u16* q16,
     }
   x->search_stats[sampled ? 0 : 3] += nq - (int64_t)overflow.size();
   if (overflow.empty()) return CLM_OK;
-  // Candidate lists beyond CAND_CAP (near-duplicate rows inside the window). Lists of up to
-  // (SORT_MAX / k) chunks are rebuilt whole by a second filter pass over just those queries and
-  // re-scored chunk-wise (overflow_wide); longer ones are redone by the exact scan, all of them in
-  // ONE scan (the index is streamed once per query block of search_scan, not once per query).
-  x->search_stats[2] += (int64_t)overflow.size();
-  std::vector<int64_t> wide, wcount, full;
-  for (size_t j = 0; j < overflow.size(); ++j) {
-    // headroom over the first pass's count: a different tile shape may round a score differently
-    const int64_t cap2 = ocount[j] + ocount[j] / 8 + 256;
-    if ((cap2 + RESCORE_WIDE_CHUNK - 1) / RESCORE_WIDE_CHUNK * k <= 8192) {
-      wide.push_back(overflow[j]);
-      wcount.push_back(cap2);
-    } else {
-      full.push_back(overflow[j]);
-    }
-  }
-  if (!wide.empty() && (r = overflow_wide(x, wide, wcount, q16, qinv, q32, qn, th, k, osc, oix, full, st))) return r;
-  if (full.empty()) return CLM_OK;
-  const int64_t no = (int64_t)full.size();
-  size_t o2 = 0;
-  auto take2 = [&](size_t bytes) { size_t o = o2; o2 = round_up(o2 + bytes, 256); return o; };
-  const size_t p_x = take2((size_t)no * 8), p_q = take2((size_t)no * dim * 4), p_n = take2((size_t)no * 8),
-               p_s = take2((size_t)no * k * 4), p_i = take2((size_t)no * k * 8);
-  if ((r = grow(&x->ws4, &x->ws4_bytes, o2))) return r;   // overflow_wide is done with it (it drains its stream)
-  uint8_t* wo = (uint8_t*)x->ws4;
-  int64_t* gx = (int64_t*)(wo + p_x);
-  float* gq = (float*)(wo + p_q);
-  double* gn = (double*)(wo + p_n);
-  float* gs = (float*)(wo + p_s);
-  int64_t* gi = (int64_t*)(wo + p_i);
-  hipError_t e = hipMemcpyAsync(gx, full.data(), (size_t)no * 8, hipMemcpyHostToDevice, st);
-  if (e == hipSuccess) e = gather_rows(q32, (int64_t)dim * 4, gx, no, (int64_t)dim * 4, gq, (int64_t)dim * 4, false, st);
-  if (e == hipSuccess) e = gather_rows(qn, 8, gx, no, 8, gn, 8, false, st);
-  r = e == hipSuccess ? search_scan(x, true, nullptr, nullptr, gq, gn, no, k, gs, gi, st)
-                      : fail(CLM_E_HIP, std::string("overflow gather: ") + hipGetErrorString(e));
-  if (r == CLM_OK) e = gather_rows(gs, (int64_t)k * 4, gx, no, (int64_t)k * 4, osc, (int64_t)k * 4, true, st);
-  if (r == CLM_OK && e == hipSuccess) e = gather_rows(gi, (int64_t)k * 8, gx, no, (int64_t)k * 8, oix, (int64_t)k * 8, true, st);
-  (void)hipStreamSynchronize(st);
+  return finish_overflow(x, overflow, ocount, q16, qinv, q32, qn, th, k, osc, oix, st);
+}
+
+// Small query batches (nq <= 16) on a large index -- the reference's own pattern, one query per
+// search_with_embedding call (search.py:93-99, seeker_service.py:183-186). The bounded search's
+// MFMA filter pads such a batch to 256-row query tiles (>= 94 % padding) and its sampled-threshold
+// phase adds a second GEMM; here the index is streamed ONCE (scan16: fp16-pass scores of every row
+// into [nq, ldo] + each 256-row chunk's maximum), then
+//  1. th[q] = (k-th largest chunk maximum of q) - RESCORE_MARGIN: k chunks whose maxima are >= the
+//     k-th largest hold k distinct rows, so it is <= the fp16-pass k-th best, a lower bound like
+//     the sampled threshold (search_bounded step 1);
+//  2. collect_ge appends every (score, row) >= th[q] (CAND_CAP per query; ~k + the rows within the
+//     margin), 4 bytes per stored score read once;
+//  3. rescore_select: exact fp64 re-score and (score desc, index asc) top k -- the same routine and
+//     bits as every other path. Lists past CAND_CAP go through finish_overflow.
+// Needs nchunk >= k (N >= 256 k) and the score matrix's offsets within one buffer descriptor.
+static bool search_small_fits(const clm_index* x, int64_t nq, int k) {
+  const int64_t N = x->n, dim = x->dim;
+  const int64_t nchunk = (N + 255) / 256, ldo = round_up(N, (int64_t)64);
+  return nq >= 1 && nq <= 16 && k >= 1 && k <= 1024 && dim >= 64 && dim <= 1024 && dim % 64 == 0 && nchunk >= k &&
+         (nq - 1) * ldo * 4 + 64 <= 0x7FFFFFF0LL && (nq - 1) * nchunk * 4 + 4 <= 0x7FFFFFF0LL;
+}
+
+static int search_small(clm_index* x, const u16* q16, const float* qinv, const float* q32, const double* qn,
+                        int64_t nq, int k, float* osc, int64_t* oix, hipStream_t st) {
+  const int dim = (int)x->dim;
+  const int64_t N = x->n;
+  const int64_t nchunk = (N + 255) / 256, ldo = round_up(N, (int64_t)64);
+  size_t off = 0;
+  auto take = [&](size_t bytes) { size_t o = off; off = round_up(off + bytes, 256); return o; };
+  const size_t o_sc = take((size_t)nq * ldo * 4);
+  const size_t o_cm = take((size_t)nq * nchunk * 4);
+  const size_t o_th = take((size_t)nq * 4);
+  const size_t o_cnt = take((size_t)nq * 4);
+  const size_t o_ts = take((size_t)nq * k * 4);
+  const size_t o_ti = take((size_t)nq * k * 8);
+  const size_t o_cs = take((size_t)nq * CAND_CAP * 4);
+  const size_t o_ci = take((size_t)nq * CAND_CAP * 8);
+  int r = grow(&x->ws2, &x->ws2_bytes, off);
   if (r) return r;
-  if (e != hipSuccess) return fail(CLM_E_HIP, std::string("overflow scatter: ") + hipGetErrorString(e));
-  return CLM_OK;
+  uint8_t* w = (uint8_t*)x->ws2;
+  float* sc = (float*)(w + o_sc);
+  float* cm = (float*)(w + o_cm);
+  float* th = (float*)(w + o_th);
+  int* cnt = (int*)(w + o_cnt);
+  Scan16Args a{};
+  a.rows = x->rows; a.inv = x->inv; a.N = N; a.dim = dim;
+  a.q16 = q16; a.qinv = qinv; a.nq = (int)nq;
+  a.out = sc; a.ldo = ldo; a.cmax = cm; a.nchunk = nchunk;
+  KCHK(scan16(a, st));
+  if (k <= 8 && !g_kth_radix) {
+    KCHK(kth_thresholds(cm, nchunk, nq, nchunk, k, RESCORE_MARGIN, th, st));
+  } else {
+    KCHK(topk_rows(cm, nchunk, nq, nchunk, k, 0, (float*)(w + o_ts), (int64_t*)(w + o_ti), k, st));
+    KCHK(filter_thresholds((const float*)(w + o_ts), k, nq, k, RESCORE_MARGIN, th, st));
+  }
+  HIPCHK(hipMemsetAsync(cnt, 0, (size_t)nq * 4, st));
+  KCHK(collect_ge(sc, ldo, nq, N, th, cnt, CAND_CAP, (float*)(w + o_cs), (int64_t*)(w + o_ci), x->offset, st));
+  const void* xrows = x->rows32 ? (const void*)x->rows32 : (const void*)x->rows;
+  KCHK(rescore_select((const float*)(w + o_cs), (const int64_t*)(w + o_ci), cnt, CAND_CAP, q32, qn, dim, xrows,
+                      !x->rows32, x->offset, RESCORE_MARGIN, nq, k, osc, oix, st));
+  std::vector<int> hcnt(nq);
+  HIPCHK(hipMemcpyAsync(hcnt.data(), cnt, (size_t)nq * 4, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
+  std::vector<int64_t> overflow, ocount;
+  for (int64_t i = 0; i < nq; ++i)
+    if (hcnt[i] > CAND_CAP) {
+      overflow.push_back(i);
+      ocount.push_back(hcnt[i]);
+    }
+  x->search_stats[6] += nq - (int64_t)overflow.size();
+  if (overflow.empty()) return CLM_OK;
+  return finish_overflow(x, overflow, ocount, q16, qinv, q32, qn, th, k, osc, oix, st);
 }
 
 // Top-k by EXACT cosine (the fp32-rounded fp64 cosine of the caller's query and rows), order
@@ -2124,7 +2127,16 @@ int clm_index_search(clm_index* x, const void* q, int q_dtype, int64_t nq, int k
   const char* e_exact = getenv("CLM_SEARCH_EXACT");
   const char* e_bounded = getenv("CLM_SEARCH_BOUNDED");   // tests: bounded search at any size
   const bool force_bounded = e_bounded && atoi(e_bounded) && N > 0;
-  if (k > 1024) {
+  // small batches on a large index: one streaming pass (search_small); $CLM_SEARCH_SMALLQ=1 takes
+  // it at any size (tests), 0 never
+  const char* e_small = getenv("CLM_SEARCH_SMALLQ");
+  const int small_mode = e_small ? atoi(e_small) : -1;
+  const bool small = small_mode != 0 && k <= 1024 && N > 0 && search_small_fits(x, nq, k) &&
+                     (small_mode == 1 || (!force_bounded && !(e_full && atoi(e_full)) && !(e_exact && atoi(e_exact)) &&
+                                          (double)nq * (double)N > (double)(1 << 24)));
+  if (small) {
+    r = search_small(x, q16, qinv, q32, qn, nq, k, osc, oix, st);
+  } else if (k > 1024) {
     // any k: the exact scan over whole rows (topk_rows / the candidate lists stop at 1024)
     r = search_scan_large(x, q32, qn, nq, k, osc, oix, st);
     x->search_stats[1] += nq;
@@ -2161,9 +2173,9 @@ int clm_index_stats(const clm_index* x, int64_t* filtered, int64_t* exact, int64
 
 int clm_index_stats2(const clm_index* x, int64_t* out, int n) {
   if (!x || !out || n < 0) return fail(CLM_E_ARG, "bad argument");
-  const int64_t v[6] = {x->search_stats[0], x->search_stats[3], x->search_stats[1], x->search_stats[2],
-                        x->search_stats[4], x->search_stats[5]};
-  for (int i = 0; i < n && i < 6; ++i) out[i] = v[i];
+  const int64_t v[7] = {x->search_stats[0], x->search_stats[3], x->search_stats[1], x->search_stats[2],
+                        x->search_stats[4], x->search_stats[5], x->search_stats[6]};
+  for (int i = 0; i < n && i < 7; ++i) out[i] = v[i];
   return CLM_OK;
 }
 

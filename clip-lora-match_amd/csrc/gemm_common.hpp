@@ -434,15 +434,15 @@ __device__ __forceinline__ void epilogue(const GemmArgs& g, const f32x4 (&acc)[B
 // Stores (vector-memory instructions) one tile's epilogue issues per wave at least, on the
 // vector paths; the main loop's counted vmcnt leaves this many in flight after a tile end
 // (a smaller count than actually issued only over-waits). FILTER stores in branches: 0.
+// EPI_SCORE with TN == 8 may run the group-maxima form (GemmArgs::out16 == 2: one 16-B store per
+// row-block, TM in all), so it counts TM.
 template <int EPI, int TM, int TN>
 constexpr int epi_min_stores() {
-  return epi_stores16(EPI) ? TM * TN / 2 : EPI == EPI_FILTER ? 0 : TM * TN;
+  return epi_stores16(EPI) ? TM * TN / 2 : EPI == EPI_FILTER ? 0 : (EPI == EPI_SCORE && TN == 8) ? TM : TM * TN;
 }
 
 }  // namespace gemm_detail
 
 // G2 kernels (k_gemm2.hip): configs 8-11
 hipError_t gemm2_launch(bool bf16, int epi, int id, const GemmArgs& g, hipStream_t s);
-hipError_t gemm2_pair_launch(bool bf0, bool bf1, int epi, int id, const GemmArgs& g0, const GemmArgs& g1,
-                             const PairGrid& pg, hipStream_t s);
 }  // namespace clm

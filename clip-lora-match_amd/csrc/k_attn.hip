@@ -619,7 +619,9 @@ __global__ __launch_bounds__(256, 4) void attn_long_dma_kernel(const u16* qkv, i
         dm = mnew - m;   // +inf on the first step: alpha = 0 scales the zero O and sum
         m = mnew;
       }
-      const float alpha = __builtin_amdgcn_exp2f(-dm);
+      // QL2E's first step: O and the sum are still zero, and dm = m_new can be below -128 (every
+      // logit of the first 32 keys under about -88.7), where exp2(-dm) is +inf and 0 * inf NaN
+      const float alpha = (QL2E && first) ? 0.f : __builtin_amdgcn_exp2f(-dm);
       l *= alpha;
 #pragma unroll
       for (int db = 0; db < 2; ++db)

@@ -22,7 +22,6 @@
 //    (and its L2 lines) run on one XCD.
 #include <algorithm>
 #include <cstdlib>
-#include <functional>
 #include <vector>
 
 #include "gemm_common.hpp"
@@ -35,8 +34,6 @@ using namespace gemm_detail;
 // K-tiles of tile i+1 are issued before tile i's epilogue, so they land while the epilogue
 // runs, and the epilogue's stores drain under tile i+1's main loop (counted vmcnt that
 // leaves them in flight). A one-tile-per-workgroup grid is the plain non-persistent GEMM.
-// The body of workgroup `bid` of the G that serve one problem (gemm_kernel: the whole grid;
-// gemm_pair_kernel: one of the two problems' ranges).
 template <bool BF, int EPI, int BM, int BN, int WM, int WN, int STAGES>
 __device__ __forceinline__ void gemm_body(const GemmArgs& ga, int bid, int G) {
   using C = Cfg<BM, BN, WM, WN, STAGES>;
@@ -225,20 +222,6 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& ga, int bid, int G) {
 template <bool BF, int EPI, int BM, int BN, int WM, int WN, int STAGES>
 __global__ __launch_bounds__(WM * WN * 64, (Cfg<BM, BN, WM, WN, STAGES>::WAVES_PER_EU)) void gemm_kernel(GemmArgs ga) {
   gemm_body<BF, EPI, BM, BN, WM, WN, STAGES>(ga, blockIdx.x, gridDim.x);
-}
-
-// Two independent problems in one launch (the two CLIP towers' layer-l GEMMs, clm_encode_pair's
-// grouped mode): workgroups [0, G0) serve g0 with operand type BF0, [n0, n0 + G1) serve g1 with
-// BF1 (n0 = G0 rounded up to a multiple of 8, so both ranges start on XCD 0 and keep their
-// XCD-aware remaps; the padding workgroups exit). With G0 / G1 = the tile counts (one tile per
-// workgroup) the hardware dispatcher hands the second problem's tiles to slots as the first
-// problem's finish, so the towers' tiles share one round structure instead of two launches'.
-template <bool BF0, bool BF1, int EPI, int BM, int BN, int WM, int WN, int STAGES>
-__global__ __launch_bounds__(WM * WN * 64, (Cfg<BM, BN, WM, WN, STAGES>::WAVES_PER_EU)) void gemm_pair_kernel(
-    GemmArgs g0, GemmArgs g1, int G0, int n0, int G1) {
-  const int b = blockIdx.x;
-  if (b < G0) gemm_body<BF0, EPI, BM, BN, WM, WN, STAGES>(g0, b, G0);
-  else if (b >= n0) gemm_body<BF1, EPI, BM, BN, WM, WN, STAGES>(g1, b - n0, G1);
 }
 
 template <bool BF, int EPI, int BM, int BN, int WM, int WN, int STAGES>
@@ -435,149 +418,5 @@ hipError_t gemm_splitk_resid(bool bf16, const GemmArgs& g, int slices, float* ws
 }
 
 void gemm_set_concurrent(bool on) { g_concurrent = on; }
-
-// ----------------------------------------------------------------- grouped (pair) launch ---
-namespace {
-int tiles_of(const GemmArgs& g, int bm, int bn) { return ((g.M + bm - 1) / bm) * ((g.N + bn - 1) / bn); }
-
-// workgroup ranges of a grouped launch over `slots` resident slots
-PairGrid pair_grid(const GemmArgs& g0, const GemmArgs& g1, int bm, int bn, int slots, int persist) {
-  const int t0 = tiles_of(g0, bm, bn), t1 = tiles_of(g1, bm, bn);
-  PairGrid pg{t0, 0, t1};
-  if (persist && t0 + t1 > slots) {   // split the slots by work (tiles x K)
-    const double w0 = (double)t0 * g0.K, w1 = (double)t1 * g1.K;
-    int G0 = (int)(slots * w0 / (w0 + w1) + 0.5);
-    G0 = std::max(1, std::min({G0, t0, slots - 1}));
-    pg.G0 = G0;
-    pg.G1 = std::max(1, std::min(t1, slots - G0));
-  }
-  pg.n0 = (pg.G0 + 7) / 8 * 8;
-  return pg;
-}
-
-template <bool BF0, bool BF1, int EPI, int BM, int BN, int WM, int WN, int STAGES>
-hipError_t launch_pair_cfg(const GemmArgs& g0, const GemmArgs& g1, int persist, hipStream_t s) {
-  using C = Cfg<BM, BN, WM, WN, STAGES>;
-  auto kern = gemm_pair_kernel<BF0, BF1, EPI, BM, BN, WM, WN, STAGES>;
-  static unsigned dev_done = 0;
-  int dev = 0;
-  (void)hipGetDevice(&dev);
-  if (!(__atomic_load_n(&dev_done, __ATOMIC_ACQUIRE) & (1u << (dev & 31)))) {
-    hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, C::LDS);
-    if (e != hipSuccess) return e;
-    __atomic_fetch_or(&dev_done, 1u << (dev & 31), __ATOMIC_RELEASE);
-  }
-  static int slots[32] = {};
-  int& sl = slots[dev & 31];
-  if (sl == 0) {
-    int per_cu = 0, cus = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, C::NT, C::LDS) != hipSuccess || per_cu < 1) per_cu = 1;
-    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1) cus = 256;
-    (void)hipGetLastError();
-    sl = per_cu * cus;
-  }
-  const PairGrid pg = pair_grid(g0, g1, BM, BN, sl, persist);
-  kern<<<dim3(pg.n0 + pg.G1), dim3(C::NT), C::LDS, s>>>(g0, g1, pg.G0, pg.n0, pg.G1);
-  return hipGetLastError();
-}
-
-int g2_slots() {
-  static int cus = 0;
-  if (cus == 0) {
-    int dev = 0;
-    (void)hipGetDevice(&dev);
-    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1) cus = 256;
-    (void)hipGetLastError();
-  }
-  return cus;
-}
-
-// configs a grouped launch instantiates: the 2-workgroup/CU tiles and 256 x 128 (gemm_kernel), and
-// the G2 family
-template <bool BF0, bool BF1, int EPI>
-hipError_t pair_by_id(int id, const GemmArgs& g0, const GemmArgs& g1, int persist, hipStream_t s) {
-  switch (id) {
-    case 0: return launch_pair_cfg<BF0, BF1, EPI, 128, 128, 2, 2, 2>(g0, g1, persist, s);
-    case 3: return launch_pair_cfg<BF0, BF1, EPI, 128, 192, 2, 2, 2>(g0, g1, persist, s);
-    case 4: return launch_pair_cfg<BF0, BF1, EPI, 192, 128, 2, 2, 2>(g0, g1, persist, s);
-    case 5: return launch_pair_cfg<BF0, BF1, EPI, 256, 128, 4, 2, 2>(g0, g1, persist, s);
-    case 7: return launch_pair_cfg<BF0, BF1, EPI, 160, 128, 2, 2, 2>(g0, g1, persist, s);
-    case 8: case 9: case 10: case 11: {
-      static const int bmn[4][2] = {{256, 192}, {256, 128}, {192, 256}, {128, 256}};
-      const PairGrid pg = pair_grid(g0, g1, bmn[id - 8][0], bmn[id - 8][1], g2_slots(), persist);
-      return gemm2_pair_launch(BF0, BF1, EPI, id, g0, g1, pg, s);
-    }
-    default: return hipErrorInvalidValue;
-  }
-}
-template <bool BF0, bool BF1>
-hipError_t pair_by_epi(int epi, int id, const GemmArgs& g0, const GemmArgs& g1, int persist, hipStream_t s) {
-  switch (epi) {
-    case EPI_RESID: return pair_by_id<BF0, BF1, EPI_RESID>(id, g0, g1, persist, s);
-    case EPI_GELU: return pair_by_id<BF0, BF1, EPI_GELU>(id, g0, g1, persist, s);
-    default: return hipErrorInvalidValue;
-  }
-}
-
-// greedy list scheduling of t0 tiles of cost c0 then t1 of cost c1 over `slots` slots
-double list_makespan(int t0, double c0, int t1, double c1, int slots) {
-  std::vector<double> heap(std::max(1, slots), 0.0);   // min-heap of slot free times
-  auto put = [&](double c) {
-    std::pop_heap(heap.begin(), heap.end(), std::greater<double>());
-    heap.back() += c;
-    std::push_heap(heap.begin(), heap.end(), std::greater<double>());
-  };
-  for (int i = 0; i < t0; ++i) put(c0);
-  for (int i = 0; i < t1; ++i) put(c1);
-  return *std::max_element(heap.begin(), heap.end());
-}
-}  // namespace
-
-int pick_pair_config(int epi, const GemmArgs& g0, const GemmArgs& g1) {
-  static int forced[2] = {-2, -2};   // $CLM_PAIR_CFG_RESID / $CLM_PAIR_CFG_GELU (A/B)
-  const int which = epi == EPI_GELU ? 1 : 0;
-  if (forced[which] == -2) {
-    const char* e = getenv(which ? "CLM_PAIR_CFG_GELU" : "CLM_PAIR_CFG_RESID");
-    forced[which] = e ? atoi(e) : -1;
-  }
-  if (forced[which] >= 0) return forced[which];
-  // candidates: RESID -> the 2-workgroup/CU tiles (the RMW epilogue of one overlaps the other's
-  // main loop); GELU -> G2 (as gemm()) and gemm_kernel 256 x 128
-  static const CfgModel resid[] = {{0, 128, 128, 2, 0.975}, {3, 128, 192, 2, 0.955}, {4, 192, 128, 2, 0.955},
-                                   {7, 160, 128, 2, 0.93}};
-  static const CfgModel gelu[] = {{8, 256, 192, 1, 2.569}, {9, 256, 128, 1, 2.349}, {10, 192, 256, 1, 2.521},
-                                  {11, 128, 256, 1, 2.340}};
-  const CfgModel* ms = which ? gelu : resid;
-  const int nm = which ? 4 : 4;
-  int best = ms[0].id;
-  double best_t = 1e300;
-  for (int i = 0; i < nm; ++i) {
-    const CfgModel& c = ms[i];
-    const double per = (double)c.bm * c.bn * c.wg_per_cu / c.eff;
-    const double t = list_makespan(tiles_of(g0, c.bm, c.bn), per * g0.K, tiles_of(g1, c.bm, c.bn), per * g1.K,
-                                   256 * c.wg_per_cu);
-    if (t < best_t * 0.999) { best_t = t; best = c.id; }
-  }
-  return best;
-}
-
-hipError_t gemm_pair(bool bf0, bool bf1, int epi, int config, const GemmArgs& g0, const GemmArgs& g1, int persist,
-                     hipStream_t s) {
-  if (g0.M <= 0 || g0.N <= 0) return gemm(bf1, epi, g1, s);
-  if (g1.M <= 0 || g1.N <= 0) return gemm(bf0, epi, g0, s);
-  for (const GemmArgs* g : {&g0, &g1})
-    if (g->K <= 0 || (g->K % 32) != 0 || (g->lda % 8) != 0 || (g->ldw % 8) != 0 || g->ksplit > 1)
-      return hipErrorInvalidValue;
-  const int id = config >= 0 ? config : pick_pair_config(epi, g0, g1);
-  if (id >= 8 && ((g0.K % BK) || (g1.K % BK))) {   // G2 needs whole K-steps: two launches
-    hipError_t e = gemm(bf0, epi, g0, s);
-    return e != hipSuccess ? e : gemm(bf1, epi, g1, s);
-  }
-  if (bf0 && !bf1) return pair_by_epi<true, false>(epi, id, g0, g1, persist, s);
-  if (bf0 == bf1) return bf0 ? pair_by_epi<true, true>(epi, id, g0, g1, persist, s)
-                             : pair_by_epi<false, false>(epi, id, g0, g1, persist, s);
-  return hipErrorInvalidValue;
-}
-
 
 }  // namespace clm

@@ -183,14 +183,6 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void gemm2_kernel(GemmArgs ga) {
   gemm2_body<BF, EPI, BM, BN, WM, WN>(ga, blockIdx.x, gridDim.x);
 }
 
-// two problems in one launch (k_gemm.hip gemm_pair_kernel's layout): [0, G0) -> g0, [n0, n0 + G1) -> g1
-template <bool BF0, bool BF1, int EPI, int BM, int BN, int WM, int WN>
-__global__ __launch_bounds__(WM * WN * 64, 1) void gemm2_pair_kernel(GemmArgs g0, GemmArgs g1, int G0, int n0, int G1) {
-  const int b = blockIdx.x;
-  if (b < G0) gemm2_body<BF0, EPI, BM, BN, WM, WN>(g0, b, G0);
-  else if (b >= n0) gemm2_body<BF1, EPI, BM, BN, WM, WN>(g1, b - n0, G1);
-}
-
 template <bool BF, int EPI, int BM, int BN, int WM, int WN>
 hipError_t launch_cfg2(const GemmArgs& g, hipStream_t s) {
   using C = Cfg2<BM, BN, WM, WN>;
@@ -238,49 +230,10 @@ hipError_t by_epi(int epi, int id, const GemmArgs& g, hipStream_t s) {
     default: return hipErrorInvalidValue;
   }
 }
-template <bool BF0, bool BF1, int EPI, int BM, int BN, int WM, int WN>
-hipError_t launch_pair2(const GemmArgs& g0, const GemmArgs& g1, const PairGrid& pg, hipStream_t s) {
-  using C = Cfg2<BM, BN, WM, WN>;
-  auto kern = gemm2_pair_kernel<BF0, BF1, EPI, BM, BN, WM, WN>;
-  static unsigned dev_done = 0;
-  int dev = 0;
-  (void)hipGetDevice(&dev);
-  if (!(__atomic_load_n(&dev_done, __ATOMIC_ACQUIRE) & (1u << (dev & 31)))) {
-    hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, C::LDS);
-    if (e != hipSuccess) return e;
-    __atomic_fetch_or(&dev_done, 1u << (dev & 31), __ATOMIC_RELEASE);
-  }
-  kern<<<dim3(pg.n0 + pg.G1), dim3(C::NT), C::LDS, s>>>(g0, g1, pg.G0, pg.n0, pg.G1);
-  return hipGetLastError();
-}
-template <bool BF0, bool BF1, int EPI>
-hipError_t pair2_by_id(int id, const GemmArgs& g0, const GemmArgs& g1, const PairGrid& pg, hipStream_t s) {
-  switch (id) {
-    case 8: return launch_pair2<BF0, BF1, EPI, 256, 192, 4, 2>(g0, g1, pg, s);
-    case 9: return launch_pair2<BF0, BF1, EPI, 256, 128, 4, 2>(g0, g1, pg, s);
-    case 10: return launch_pair2<BF0, BF1, EPI, 192, 256, 2, 4>(g0, g1, pg, s);
-    case 11: return launch_pair2<BF0, BF1, EPI, 128, 256, 2, 4>(g0, g1, pg, s);
-    default: return hipErrorInvalidValue;
-  }
-}
-template <bool BF0, bool BF1>
-hipError_t pair2_by_epi(int epi, int id, const GemmArgs& g0, const GemmArgs& g1, const PairGrid& pg, hipStream_t s) {
-  switch (epi) {
-    case EPI_GELU: return pair2_by_id<BF0, BF1, EPI_GELU>(id, g0, g1, pg, s);
-    case EPI_RESID: return pair2_by_id<BF0, BF1, EPI_RESID>(id, g0, g1, pg, s);
-    default: return hipErrorInvalidValue;
-  }
-}
 }  // namespace
 
 hipError_t gemm2_launch(bool bf16, int epi, int id, const GemmArgs& g, hipStream_t s) {
   return bf16 ? by_epi<true>(epi, id, g, s) : by_epi<false>(epi, id, g, s);
 }
 
-hipError_t gemm2_pair_launch(bool bf0, bool bf1, int epi, int id, const GemmArgs& g0, const GemmArgs& g1,
-                             const PairGrid& pg, hipStream_t s) {
-  if (bf0 && !bf1) return pair2_by_epi<true, false>(epi, id, g0, g1, pg, s);
-  if (bf0 == bf1) return bf0 ? pair2_by_epi<true, true>(epi, id, g0, g1, pg, s) : pair2_by_epi<false, false>(epi, id, g0, g1, pg, s);
-  return hipErrorInvalidValue;   // (fp16, bf16): the callers put the bf16 vision tower first
-}
 }  // namespace clm

@@ -296,34 +296,6 @@ __global__ __launch_bounds__(FA_NW * 64, 2) void gemm_attn_kernel(FaArgs a) {
   gemm_attn_body<BF, CAUSAL, VL>(a, blockIdx.x, gridDim.x);
 }
 
-// the two towers' layer-l q/k/v + attention in one launch: workgroups [0, n0p) serve a0 (the
-// image tower: non-causal, fixed length; n0p = its tile count rounded up to a multiple of 8, the
-// padding exits), [n0p, n0p + n1) serve a1 (the causal text tower, varlen or not). One tile per
-// workgroup, the larger image tiles first: the dispatcher fills the slots the image tiles free
-// with caption tiles, so the two launches' partial last rounds become one.
-template <bool BF0, bool BF1, bool VL1>
-__global__ __launch_bounds__(FA_NW * 64, 2) void gemm_attn_pair_kernel(FaArgs a0, FaArgs a1, int n0, int n0p, int n1) {
-  const int b = blockIdx.x;
-  if (b < n0) gemm_attn_body<BF0, false, false>(a0, b, n0);
-  else if (b >= n0p) gemm_attn_body<BF1, true, VL1>(a1, b - n0p, n1);
-}
-
-template <bool BF0, bool BF1, bool VL1>
-hipError_t launch_pair(const FaArgs& a0, int n0, const FaArgs& a1, int n1, hipStream_t s) {
-  auto kern = gemm_attn_pair_kernel<BF0, BF1, VL1>;
-  static unsigned dev_done = 0;
-  int dev = 0;
-  (void)hipGetDevice(&dev);
-  if (!(__atomic_load_n(&dev_done, __ATOMIC_ACQUIRE) & (1u << (dev & 31)))) {
-    hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, FA_LDS);
-    if (e != hipSuccess) return e;
-    __atomic_fetch_or(&dev_done, 1u << (dev & 31), __ATOMIC_RELEASE);
-  }
-  const int n0p = (n0 + 7) / 8 * 8;
-  kern<<<dim3(n0p + n1), dim3(FA_NW * 64), FA_LDS, s>>>(a0, a1, n0, n0p, n1);
-  return hipGetLastError();
-}
-
 template <bool BF, bool CAUSAL, bool VL>
 hipError_t launch(const FaArgs& a, int tiles, hipStream_t s) {
   auto kern = gemm_attn_kernel<BF, CAUSAL, VL>;
@@ -398,19 +370,6 @@ hipError_t gemm_attn_varlen(bool bf16, bool causal, const u16* X, int64_t ldx, c
   if (!varlen_args(p, a, grid)) return hipErrorInvalidValue;
   if (bf16) return causal ? launch<true, true, true>(a, grid, s) : launch<true, false, true>(a, grid, s);
   return causal ? launch<false, true, true>(a, grid, s) : launch<false, false, true>(a, grid, s);
-}
-
-hipError_t gemm_attn_pair(bool bf0, bool bf1, const AttnProblem& img, const AttnProblem& txt, hipStream_t s) {
-  if (img.B <= 0 || txt.B <= 0) return hipErrorInvalidValue;
-  FaArgs a0, a1;
-  int n0, n1;
-  const bool vl = txt.lens != nullptr;
-  if (!fixed_args(img, a0, n0) || !(vl ? varlen_args(txt, a1, n1) : fixed_args(txt, a1, n1)))
-    return hipErrorInvalidValue;
-  if (bf0 && !bf1) return vl ? launch_pair<true, false, true>(a0, n0, a1, n1, s) : launch_pair<true, false, false>(a0, n0, a1, n1, s);
-  if (bf0 && bf1) return vl ? launch_pair<true, true, true>(a0, n0, a1, n1, s) : launch_pair<true, true, false>(a0, n0, a1, n1, s);
-  if (!bf0 && !bf1) return vl ? launch_pair<false, false, true>(a0, n0, a1, n1, s) : launch_pair<false, false, false>(a0, n0, a1, n1, s);
-  return hipErrorInvalidValue;
 }
 
 }  // namespace clm

@@ -205,26 +205,6 @@ __global__ __launch_bounds__(256) void ln4_kernel(LnArgs a) {
   ln4_body<BF, NQ, R>(a, blockIdx.x);
 }
 
-// the two towers' LayerNorms of one layer in one launch: blocks [0, nb0) normalise a0's rows
-// (image tower, d = 256 NQ0), the rest a1's (text tower, d = 256 NQ1); each row exactly as
-// ln4_kernel computes it
-template <bool BF0, int NQ0, bool BF1, int NQ1>
-__global__ __launch_bounds__(256) void ln4_pair_kernel(LnArgs a0, LnArgs a1, int nb0) {
-  const int b = blockIdx.x;
-  if (b < nb0) ln4_body<BF0, NQ0>(a0, b);
-  else ln4_body<BF1, NQ1>(a1, b - nb0);
-}
-
-template <bool BF0, bool BF1>
-hipError_t ln_pair_dims(const LnArgs& a0, const LnArgs& a1, hipStream_t s) {
-  const int nb0 = (a0.M + 7) / 8, nb1 = (a1.M + 7) / 8;
-  if (a0.d == 768 && a1.d == 512) ln4_pair_kernel<BF0, 3, BF1, 2><<<nb0 + nb1, 256, 0, s>>>(a0, a1, nb0);
-  else if (a0.d == 1024 && a1.d == 768) ln4_pair_kernel<BF0, 4, BF1, 3><<<nb0 + nb1, 256, 0, s>>>(a0, a1, nb0);
-  else if (a0.d == 512 && a1.d == 512) ln4_pair_kernel<BF0, 2, BF1, 2><<<nb0 + nb1, 256, 0, s>>>(a0, a1, nb0);
-  else return hipErrorNotSupported;
-  return hipGetLastError();
-}
-
 template <bool BF>
 hipError_t ln_dispatch(const LnArgs& a, hipStream_t s) {
   dim3 grid((a.M + 3) / 4), block(256);
@@ -648,19 +628,6 @@ hipError_t layernorm(bool bf16, const LnArgs& a, hipStream_t s) {
   if (a.M <= 0) return hipSuccess;
   return bf16 ? ln_dispatch<true>(a, s) : ln_dispatch<false>(a, s);
 }
-
-hipError_t layernorm_pair(bool bf0, bool bf1, const LnArgs& a0, const LnArgs& a1, hipStream_t s) {
-  if (a0.M <= 0) return layernorm(bf1, a1, s);
-  if (a1.M <= 0) return layernorm(bf0, a0, s);
-  hipError_t e = hipErrorNotSupported;
-  if (bf0 && !bf1) e = ln_pair_dims<true, false>(a0, a1, s);
-  else if (bf0 && bf1) e = ln_pair_dims<true, true>(a0, a1, s);
-  else if (!bf0 && !bf1) e = ln_pair_dims<false, false>(a0, a1, s);
-  if (e != hipErrorNotSupported) return e;
-  e = layernorm(bf0, a0, s);   // other widths: two launches
-  return e != hipSuccess ? e : layernorm(bf1, a1, s);
-}
-
 
 hipError_t patchify(bool bf16, const void* pix, int layout, int B, int S, int p, int C, const float* lut,
                     u16* P, int Kp, hipStream_t s) {

@@ -931,4 +931,248 @@ hipError_t f16_to_f32_rows(const u16* src, int64_t n, int dim, float* dst, hipSt
   return hipGetLastError();
 }
 
+namespace {
+// ------------------------------------------------------------------------------------------
+// Small query batches (nq <= 16) against a large index: the reference's own call pattern, one
+// query per search_with_embedding call (src/embedding/search.py:93-99, seeker_service.py:183-186).
+// The MFMA filter GEMM pads such a batch to 256-row query tiles; this pass streams the fp16 index
+// once at HBM rate instead (10.24 GB for configs[4]'s 10 M x 512), every wave on its own rows:
+//  * the index is cut into chunks of 256 rows; wave w of the W in the grid takes chunks w, w + W,
+//    ... (each 256 x dim x 2 bytes contiguous), 16-row blocks through a per-wave D-deep LDS ring
+//    filled by buffer_load ... lds (one 1 KiB wave-instruction per 512 row bytes, whole rows, the
+//    16-B chunks XOR-swizzled on the source so the fragment reads are conflict-free) plus one DMA of
+//    the block's 16 inverse norms. No barriers: a wave reads only the blocks it loaded;
+//  * per block, dim / 32 v_mfma_f32_16x16x32_f16 with the index rows on the A port and the (<= 16)
+//    unit-rounded fp16 queries held in registers on the B port: lane l ends with rows 4 (l >> 4) ..
+//    +3 of query l & 15, scored as the EPI_SCORE epilogue does (acc * qinv[q] * inv[row]), stored
+//    16 B per lane into the [nq, ldo] score matrix, and max-reduced into the chunk's maximum;
+//  * cmax[q][chunk] = the largest fp16-pass score of the chunk (NaN scores ignored, rows past N
+//    -inf). The k-th largest chunk maximum is at most the k-th largest score of the whole index
+//    (k chunks whose maxima reach it hold k distinct rows), so th = that - margin bounds the
+//    candidates exactly as the sampled threshold does (capi.cpp search_small).
+// Counted vmcnt: in the steady state the DMA of block i is older than one score store and D - 2
+// (DMA + store) groups; the first and last D - 1 blocks, and the extra chunk-maximum stores, only
+// ever make the wait longer (vmcnt(0) there).
+constexpr int SCAN_CHUNK = 256;
+template <int KS, int D>
+__device__ __forceinline__ void scan16_body(const Scan16Args& a) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  typedef __attribute__((address_space(3))) void* lds_ptr_t;
+  constexpr int RB = KS * 64;            // row bytes (dim = 32 KS)
+  constexpr int BLK = 16 * RB + 1024;    // a block's LDS image: 16 rows, then its inverse norms
+  constexpr int F0 = 1 + (D - 2) * (KS + 2);
+  constexpr int F = F0 > 63 ? 63 : F0;
+  const int lane = threadIdx.x & 63, g = lane >> 4, qj = lane & 15;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int nw = blockDim.x >> 6;
+  const int64_t W = (int64_t)gridDim.x * nw;
+  const int64_t w = (int64_t)blockIdx.x * nw + wid;
+  const int64_t nchunk = a.nchunk;
+  const int64_t my = w < nchunk ? (nchunk - 1 - w) / W + 1 : 0;
+  const int64_t nb = my * (SCAN_CHUNK / 16);
+  if (nb == 0) return;
+  uint8_t* ring = smem + wid * D * BLK;
+  // chunk swizzle: 16 consecutive rows at one chunk position land on 16 distinct bank quads
+  auto sw = [](int r) { return RB >= 256 ? (r & 15) : ((r >> 1) & 7); };
+  u32x4 qf[KS];   // B port: query qj, dims (4 s + g) * 8 .. + 7
+  {
+    const u16* qp = a.q16 + (int64_t)min(qj, a.nq - 1) * (KS * 32) + g * 8;
+#pragma unroll
+    for (int s = 0; s < KS; ++s) qf[s] = qj < a.nq ? *(const u32x4*)(qp + s * 32) : u32x4{0u, 0u, 0u, 0u};
+  }
+  const float qs = qj < a.nq ? a.qinv[qj] : 0.f;
+  uint32_t doff[KS];   // DMA: instruction t, lane -> LDS slot t * 1 KiB + 16 lane of the block image
+#pragma unroll
+  for (int t = 0; t < KS; ++t) {
+    const int o = t * 1024 + lane * 16, r = o / RB, p = (o % RB) / 16;
+    doff[t] = (uint32_t)(r * RB + ((p ^ sw(r)) * 16));
+  }
+  const uint32_t ioff = lane < 4 ? (uint32_t)lane * 16 : BUF_OOB;
+  uint32_t foff[KS];   // A port: row qj of the block, chunk 4 s + g
+#pragma unroll
+  for (int s = 0; s < KS; ++s) foff[s] = (uint32_t)(qj * RB + (((4 * s + g) ^ sw(qj)) * 16));
+  auto row0_of = [&](int64_t i) { return (w + (i >> 4) * W) * SCAN_CHUNK + (i & 15) * 16; };
+  auto issue = [&](int64_t i, int buf) {
+    const int64_t r0 = row0_of(i);
+    const int left = (int)max<int64_t>(0, min<int64_t>(16, a.N - r0));
+    const auto rs = buf_rsrc(a.rows + r0 * (KS * 32), left * RB);
+    const auto ri = buf_rsrc(a.inv + r0, left * 4);
+    uint8_t* base = ring + buf * BLK;
+#pragma unroll
+    for (int t = 0; t < KS; ++t)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_ptr_t)(base + t * 1024), 16, doff[t], 0, 0, 0);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(ri, (lds_ptr_t)(base + 16 * RB), 16, ioff, 0, 0, 0);
+  };
+#pragma unroll
+  for (int j = 0; j < D - 1; ++j)
+    if (j < nb) issue(j, j);
+  float run = -INFINITY;
+  int buf = 0;
+  for (int64_t i = 0; i < nb; ++i) {
+    if (i < D - 1 || i > nb - D) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(F) : "memory");
+    // the buffer of block i - 1 is free: its fragment reads were consumed by last block's MFMAs
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if (i + D - 1 < nb) issue(i + D - 1, buf == 0 ? D - 1 : buf - 1);
+    const uint8_t* blk = ring + buf * BLK;
+    u32x4 af[KS];
+#pragma unroll
+    for (int s = 0; s < KS; ++s) af[s] = *(const u32x4*)(blk + foff[s]);
+    // the inverse norms through an asm read: the compiler's LDS-DMA alias tracking put a vmcnt(0)
+    // (every DMA in flight, the whole ring) in front of this read when it was a plain load
+    u32x4 ivr;
+    asm volatile("ds_read_b128 %0, %1" : "=v"(ivr) : "v"((uint32_t)(uintptr_t)(blk + 16 * RB + g * 16)) : "memory");
+    f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < KS; ++s) acc = mfma16<false>(af[s], qf[s], acc);
+    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(ivr));
+    const float4 iv = make_float4(__uint_as_float(ivr[0]), __uint_as_float(ivr[1]), __uint_as_float(ivr[2]),
+                                  __uint_as_float(ivr[3]));
+    const int64_t r0 = row0_of(i);
+    const int64_t rb = r0 + g * 4;   // the lane's first row
+    const float ivv[4] = {iv.x, iv.y, iv.z, iv.w};
+    float v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) v[u] = rb + u < a.N ? acc[u] * qs * ivv[u] : -INFINITY;
+    run = fmaxf(run, fmaxf(fmaxf(v[0], v[1]), fmaxf(v[2], v[3])));
+    const auto ob = buf_rsrc(a.out + r0);
+    const uint32_t oo = (qj < a.nq && rb < a.N) ? (uint32_t)(((int64_t)qj * a.ldo + g * 4) * 4) : BUF_OOB;
+    __builtin_amdgcn_raw_buffer_store_b128(u32x4{__float_as_uint(v[0]), __float_as_uint(v[1]), __float_as_uint(v[2]),
+                                                 __float_as_uint(v[3])}, ob, oo, 0, 0);
+    if ((i & 15) == 15) {   // chunk end: its maximum per query (lanes l, l ^ 16, l ^ 32, l ^ 48)
+      const float m = cross_rows_reduce<true>(run);
+      const int64_t chunk = w + (i >> 4) * W;
+      const auto cb = buf_rsrc(a.cmax + chunk);
+      const uint32_t co = (g == 0 && qj < a.nq) ? (uint32_t)((int64_t)qj * nchunk * 4) : BUF_OOB;
+      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(m), cb, co, 0, 0);
+      run = -INFINITY;
+    }
+    buf = buf + 1 == D ? 0 : buf + 1;
+  }
+}
+
+// (the body lives in a __device__ function: written inline in the kernel, hipcc's host pass left
+// every instantiation's launch stub undefined)
+template <int KS, int D>
+__global__ __launch_bounds__(256, 1) void scan16_kernel(Scan16Args a) {
+  scan16_body<KS, D>(a);
+}
+
+// candidates of the small-batch search: every (score, global row) of row q of S [nq, lds] at or
+// above th[q], appended to q's list (capacity cap; cnt[q] counts them all, so cnt > cap marks an
+// overflow). The list order is the atomics' (rescore_select sorts by (score, index)).
+__global__ __launch_bounds__(256) void collect_ge_kernel(const float* S, int64_t lds, int64_t C, const float* th,
+                                                         int* cnt, int cap, float* cs, int64_t* ci, int64_t base) {
+  const int64_t q = blockIdx.y;
+  const float t = th[q];
+  const float* s = S + q * lds;
+  for (int64_t j4 = (int64_t)blockIdx.x * 256 + threadIdx.x; j4 * 4 < C; j4 += (int64_t)gridDim.x * 256) {
+    const float4 v4 = *(const float4*)(s + j4 * 4);
+    const float v[4] = {v4.x, v4.y, v4.z, v4.w};
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int64_t j = j4 * 4 + u;
+      if (j < C && v[u] >= t) {
+        const int slot = atomicAdd(cnt + q, 1);
+        if (slot < cap) {
+          cs[q * cap + slot] = v[u];
+          ci[q * cap + slot] = base + j;
+        }
+      }
+    }
+  }
+}
+
+template <int KS, int D>
+hipError_t scan16_launch(const Scan16Args& a, int nw, hipStream_t st) {
+  auto kern = scan16_kernel<KS, D>;
+  const int lds = nw * D * (16 * KS * 64 + 1024);
+  static unsigned dev_done = 0;
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  if (!(__atomic_load_n(&dev_done, __ATOMIC_ACQUIRE) & (1u << (dev & 31)))) {
+    hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    if (e != hipSuccess) return e;
+    __atomic_fetch_or(&dev_done, 1u << (dev & 31), __ATOMIC_RELEASE);
+  }
+  static int cus_of[32] = {};
+  int& cus = cus_of[dev & 31];
+  if (cus == 0) {
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1) cus = 256;
+    (void)hipGetLastError();
+  }
+  const int64_t waves_needed = a.nchunk;
+  const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(cus, (waves_needed + nw - 1) / nw));
+  kern<<<dim3(grid), dim3(nw * 64), lds, st>>>(a);
+  return hipGetLastError();
+}
+
+template <int KS>
+hipError_t scan16_depth(const Scan16Args& a, int nw, int depth, hipStream_t st) {
+  switch (depth) {
+    case 2: return scan16_launch<KS, 2>(a, nw, st);
+    case 3: return scan16_launch<KS, 3>(a, nw, st);
+    case 4: return scan16_launch<KS, 4>(a, nw, st);
+    default: return hipErrorInvalidValue;
+  }
+}
+}  // namespace
+
+// waves per workgroup and ring depth for a row width: the most blocks in flight per CU that the
+// 160 KiB of LDS holds (NW x (D - 1)), fewer waves first on a tie; $CLM_SCAN_NW / $CLM_SCAN_D (A/B)
+void scan16_shape(int dim, int* nw, int* depth) {
+  const int blk = 16 * dim * 2 + 1024;
+  static const int env_nw = getenv("CLM_SCAN_NW") ? atoi(getenv("CLM_SCAN_NW")) : 0;
+  static const int env_d = getenv("CLM_SCAN_D") ? atoi(getenv("CLM_SCAN_D")) : 0;
+  int best_w = 0, best_d = 0, best = -1;
+  for (int d = 2; d <= 4; ++d)
+    for (int w = 1; w <= 4; ++w) {
+      if ((env_nw && w != env_nw) || (env_d && d != env_d) || w * d * blk > 160 * 1024) continue;
+      const int f = w * (d - 1);
+      if (f > best) { best = f; best_w = w; best_d = d; }
+    }
+  *nw = best_w;
+  *depth = best_d;
+}
+
+hipError_t scan16(const Scan16Args& a, hipStream_t st) {
+  if (a.N <= 0 || a.nq <= 0) return hipSuccess;
+  if (a.nq > 16 || a.dim % 64 || a.dim < 64 || a.dim > 1024 || a.ldo % 4 || a.ldo < a.N ||
+      (int64_t)(a.nq - 1) * a.ldo * 4 + 64 > 0x7FFFFFF0 || (int64_t)(a.nq - 1) * a.nchunk * 4 + 4 > 0x7FFFFFF0 ||
+      a.nchunk != (a.N + SCAN_CHUNK - 1) / SCAN_CHUNK)
+    return hipErrorInvalidValue;
+  int nw = 0, d = 0;
+  scan16_shape(a.dim, &nw, &d);
+  if (nw < 1) return hipErrorInvalidValue;
+  switch (a.dim / 32) {
+    case 2: return scan16_depth<2>(a, nw, d, st);
+    case 4: return scan16_depth<4>(a, nw, d, st);
+    case 6: return scan16_depth<6>(a, nw, d, st);
+    case 8: return scan16_depth<8>(a, nw, d, st);
+    case 10: return scan16_depth<10>(a, nw, d, st);
+    case 12: return scan16_depth<12>(a, nw, d, st);
+    case 14: return scan16_depth<14>(a, nw, d, st);
+    case 16: return scan16_depth<16>(a, nw, d, st);
+    case 18: return scan16_depth<18>(a, nw, d, st);
+    case 20: return scan16_depth<20>(a, nw, d, st);
+    case 22: return scan16_depth<22>(a, nw, d, st);
+    case 24: return scan16_depth<24>(a, nw, d, st);
+    case 26: return scan16_depth<26>(a, nw, d, st);
+    case 28: return scan16_depth<28>(a, nw, d, st);
+    case 30: return scan16_depth<30>(a, nw, d, st);
+    case 32: return scan16_depth<32>(a, nw, d, st);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+hipError_t collect_ge(const float* scores, int64_t lds, int64_t nq, int64_t C, const float* th, int* cnt, int cap,
+                      float* cs, int64_t* ci, int64_t base, hipStream_t s) {
+  if (nq <= 0 || C <= 0) return hipSuccess;
+  if ((lds & 3) || ((uintptr_t)scores & 15) || nq > 65535) return hipErrorInvalidValue;
+  const int64_t n4 = (C + 3) / 4;
+  const unsigned gx = (unsigned)std::max<int64_t>(1, std::min<int64_t>((n4 + 255) / 256, 2048));
+  collect_ge_kernel<<<dim3(gx, (unsigned)nq), 256, 0, s>>>(scores, lds, C, th, cnt, cap, cs, ci, base);
+  return hipGetLastError();
+}
+
 }  // namespace clm

@@ -71,20 +71,6 @@ int gemm_num_configs();
 // other stream; alone, the slot-filling 160x128 tiles are faster (profiles/r02_v4_gemm_160x128.txt)
 void gemm_set_concurrent(bool on);
 
-// Grouped launch of two independent GEMMs with one epilogue (EPI_RESID or EPI_GELU): the two
-// CLIP towers' layer-l out_proj / fc1 / fc2 (clm_encode_pair, grouped mode). Workgroups [0, G0)
-// run g0 (operand type bf0), [n0, n0 + G1) run g1 (bf1); each range walks its own problem's tiles
-// exactly as gemm() would, so every output bit equals the separate launches'. (bf0, bf1) =
-// (bf16, fp16) is the mixed assignment; (fp16, bf16) is not instantiated. No split-K.
-struct PairGrid { int G0, n0, G1; };
-// config < 0: pick_pair_config; persist: 0 = one tile per workgroup (the dispatcher balances the
-// two problems' tiles over the slots), 1 = persistent ranges splitting the slots by work
-hipError_t gemm_pair(bool bf0, bool bf1, int epi, int config, const GemmArgs& g0, const GemmArgs& g1, int persist,
-                     hipStream_t s);
-// tile configuration of a grouped launch: greedy list-scheduling makespan of both problems' tiles
-// over the config's slots (tiles in launch order, per-tile cost BM * BN * K / efficiency)
-int pick_pair_config(int epi, const GemmArgs& g0, const GemmArgs& g1);
-
 // ----------------------------------------------------------- row ops -------
 // LayerNorm over rows of a fp32 matrix, one wave per row.
 //   mode 0: x = src rows                         (src = h)
@@ -106,9 +92,6 @@ struct LnArgs {
   const int* m_dev; const int* rowmap;
 };
 hipError_t layernorm(bool bf16, const LnArgs& a, hipStream_t s);
-// the image and text towers' LayerNorms of one layer in one launch (d0 / d1 = 768 / 512 or
-// 1024 / 768; other widths run as two launches), rows bit-identical to layernorm()
-hipError_t layernorm_pair(bool bf0, bool bf1, const LnArgs& a0, const LnArgs& a1, hipStream_t s);
 
 // shortest-edge bicubic resize + centre crop (k_image.hip), PIL / CLIPImageProcessor arithmetic.
 // Per image: source HWC RGB bytes at src + src_off (row stride 3 W); the crop needs source rows
@@ -177,15 +160,12 @@ hipError_t gemm_attn(bool bf16, bool causal, const u16* X, int64_t ldx, const u1
 hipError_t gemm_attn_varlen(bool bf16, bool causal, const u16* X, int64_t ldx, const u16* W, int64_t ldw,
                             const float* bias, u16* out, int64_t ldo, int B, int L, int H, int d, int K,
                             const int* lens, const int* offs, const int* tiles, const int* counts, hipStream_t s);
-// one problem of a grouped (two-tower) fused q/k/v + attention launch; lens == null: fixed length T
+// one fused q/k/v + attention problem (gemm_attn / gemm_attn_varlen); lens == null: fixed length T
 struct AttnProblem {
   const u16* X; int64_t ldx; const u16* W; int64_t ldw; const float* bias; u16* out; int64_t ldo;
   int B, T, H, d, K;
   const int *lens, *offs, *tiles, *counts;   // varlen (text_plan) or null
 };
-// image tower (non-causal, fixed T) + text tower (causal; varlen if txt.lens) in one launch,
-// bit-identical to gemm_attn / gemm_attn_varlen of each; (bf0, bf1) != (fp16, bf16)
-hipError_t gemm_attn_pair(bool bf0, bool bf1, const AttnProblem& img, const AttnProblem& txt, hipStream_t s);
 
 // ----------------------------------------------------------- search --------
 // rows f32|f16 [n, dim] -> fp16 dst + fp32 inverse norms of the fp16-rounded rows
@@ -254,6 +234,23 @@ hipError_t kth_thresholds(const float* scores, int64_t lds, int64_t nq, int64_t 
 // keys[0] / keys[1] = order key (float_key) of min / max over v[0, n); a NaN anywhere makes the
 // decoded min or max NaN. keys: 2 device u32
 hipError_t value_bounds(const float* v, int64_t n, unsigned* keys, hipStream_t s);
+// small-batch search scan (k_search.hip scan16_kernel): nq <= 16 unit-rounded fp16 queries q16
+// [nq, dim] (inverse norms qinv) against the fp16 index rows [N, dim] (inverse norms inv), one
+// streaming pass: out [nq, ldo] = fp16-pass scores (acc * qinv * inv, -inf past N inside ldo),
+// cmax [nq, nchunk] = each 256-row chunk's largest score (nchunk = ceil(N / 256));
+// dim % 64 == 0, 64 <= dim <= 1024
+struct Scan16Args {
+  const u16* rows; const float* inv; int64_t N; int dim;
+  const u16* q16; const float* qinv; int nq;
+  float* out; int64_t ldo;
+  float* cmax; int64_t nchunk;
+};
+hipError_t scan16(const Scan16Args& a, hipStream_t s);
+void scan16_shape(int dim, int* nw, int* depth);
+// append every (score, base + column) of row q of scores [nq, lds] (C columns) at or above th[q]
+// to q's candidate list [cap] (cnt[q] counts them all)
+hipError_t collect_ge(const float* scores, int64_t lds, int64_t nq, int64_t C, const float* th, int* cnt, int cap,
+                      float* cs, int64_t* ci, int64_t base, hipStream_t s);
 __host__ __device__ inline unsigned float_key(float f) {
   const unsigned b = __builtin_bit_cast(unsigned, f);
   return (b & 0x80000000u) ? ~b : (b | 0x80000000u);

@@ -171,9 +171,8 @@ class ClipLoraModel:
         return oi, ot
 
     def pair_path(self) -> str:
-        """how the last encode_pair ran: "grouped" (one launch per op for both towers' layer),
-        "streams" (a stream per tower piece) or "none"."""
-        return {1: "grouped", 0: "streams"}.get(C.lib().clm_pair_path(self._ctx), "none")
+        """how the last encode_pair ran: "streams" (a stream per tower piece) or "none" (no call yet)"""
+        return {0: "streams"}.get(C.lib().clm_pair_path(self._ctx), "none")
 
     # ------------------------------------------------------------ timing --
     def prof_enable(self, enable: bool = True) -> None:

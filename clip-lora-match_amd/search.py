@@ -184,11 +184,12 @@ class CosineIndex:
         scan (`full_exact`), their sum `exact`, overflow re-runs, and the queries whose filter
         pass ran on the G2 256 x 192 tiles (`filter_g2`) or, in blocks whose sampled candidate
         windows mostly exceed the list capacity, on gemm_kernel 256 x 256 (`filter_dense`)
-        (include/clm.h)"""
-        v = (ctypes.c_int64 * 6)()
-        C.check(C.lib().clm_index_stats2(self._h, v, 6))
+        (include/clm.h), and the small batches (nq <= 16) served by the one-pass streaming search
+        (`small_scan`)"""
+        v = (ctypes.c_int64 * 7)()
+        C.check(C.lib().clm_index_stats2(self._h, v, 7))
         return {"filtered": v[0], "scan_bounded": v[1], "full_exact": v[2], "exact": v[1] + v[2],
-                "overflow": v[3], "filter_g2": v[4], "filter_dense": v[5]}
+                "overflow": v[3], "filter_g2": v[4], "filter_dense": v[5], "small_scan": v[6]}
 
     def close(self) -> None:
         if getattr(self, "_h", None):
@@ -284,10 +285,26 @@ class TextSearchIndex:
         if self.num_items:
             self._gpu.append(self.embeddings)
 
+    @classmethod
+    def from_gpu_index(cls, index: "CosineIndex", image_paths: Sequence[str] = (),
+                       texts: Sequence[str] = ()) -> "TextSearchIndex":
+        """Wrap an HBM-resident CosineIndex (e.g. one built by index_build or load_shard) as a
+        TextSearchIndex without a host copy of its rows: searches go straight to the GPU index;
+        the host mirror (`embeddings`, used by save / append) is read back from HBM on first use."""
+        self = cls.__new__(cls)
+        self._gpu = index
+        n = len(index)
+        self._host, self._n = None, n
+        self.num_items, self.dim = n, index.dim
+        self.image_paths, self.texts = list(image_paths), list(texts)
+        return self
+
     # host mirror of the rows: a capacity-doubling buffer, so append is amortised O(1) (the
     # reference's FinderService torch.cat's the whole index per report, finder_service.py:180)
     @property
     def embeddings(self) -> torch.Tensor:
+        if self._host is None:   # from_gpu_index: the rows as the index keeps them, fetched once
+            self._host = self._gpu.read(0, self._n).float()[:, : self.dim].contiguous()
         return self._host[: self._n]
 
     @embeddings.setter
@@ -343,6 +360,8 @@ class TextSearchIndex:
         if e.dim() != 2 or e.shape[1] != self.dim:
             raise ValueError(f"embedding dim {e.shape[-1]} != index dim {self.dim}")
         e = e / e.norm(dim=-1, keepdim=True)
+        if self._host is None:
+            self.embeddings   # noqa: B018 -- materialise the host mirror before growing it
         n_new = self._n + e.shape[0]
         if n_new > self._host.shape[0]:
             cap = max(n_new, 2 * self._host.shape[0], 1024)

@@ -147,12 +147,12 @@ enum { CLM_PAIR_GRAPH = 1, CLM_PAIR_SPLIT_SHIFT = 8 };
 int clm_encode_pair(clm_ctx* ctx, const void* pixels, int pix_layout, int n_img, const int32_t* ids,
                     int n_txt, int L, void* out_img, void* out_txt, int out_dtype, int normalize,
                     int flags, void* stream);
-/* How the last clm_encode_pair ran: 0 = one stream per tower piece (default), 1 = grouped
- * (opt-in: env CLM_PAIR_GROUPED=1 or clm_debug_set bit 64; S = 1 and both towers with the same
- * layer count: each layer's ops of both towers as one launch per op), -1 = no call yet. */
+/* How the last clm_encode_pair ran: 0 = one stream per tower piece (the only path; round 5's
+ * opt-in grouped launches measured 11 % slower and were removed), -1 = no call yet. */
 int clm_pair_path(const clm_ctx* ctx);
 
-/* GPU-resident cosine index (dim % 64 == 0, <= 1024). Scores are the EXACT cosine of the
+/* GPU-resident cosine index (dim % 64 == 0, <= 65536; rows wider than 8192 are always searched by
+ * the exact scan, MARGIN_MAX_DIM in capi.cpp). Scores are the EXACT cosine of the
  * caller's query and rows (fp64 arithmetic, rounded once to fp32): an fp16 MFMA pass bounds the
  * candidates, which are then re-scored against the rows as given. */
 int clm_index_create(int hip_device, int64_t capacity, int dim, clm_index** out);
@@ -192,9 +192,11 @@ int clm_index_search(clm_index* idx, const void* q, int q_dtype, int64_t nq, int
  * bounded queries whose candidate list overflowed (redone by a whole-list pass, or by the exact
  * scan when the list is longer than 8192 / k chunks of 4096) */
 int clm_index_stats(const clm_index* idx, int64_t* filtered, int64_t* exact, int64_t* overflow);
-/* out[0..n), n <= 6: sampled bounded, fp16-scan bounded, full exact scan, overflow re-runs, then the
+/* out[0..n), n <= 7: sampled bounded, fp16-scan bounded, full exact scan, overflow re-runs, then the
  * sampled queries whose filter pass ran on the G2 256 x 192 tiles / on gemm_kernel 256 x 256 (chosen
- * per query block from the block's sampled candidate counts: near-duplicate blocks take the latter) */
+ * per query block from the block's sampled candidate counts: near-duplicate blocks take the latter),
+ * then the queries served by the small-batch streaming search (nq <= 16 on a large index: one pass
+ * over the fp16 rows, thresholds from 256-row chunk maxima) */
 int clm_index_stats2(const clm_index* idx, int64_t* out, int n);
 
 /* full cosine matrix, exact: out [nq, n] f32 = fp32(cos64(q_i, c_j)), any dim */
@@ -223,6 +225,13 @@ int clm_gemm(int hip_device, int dtype, int epilogue, int config, const void* A,
              const void* W, int64_t ldw, int M, int N, int K, void* out, int64_t ldo,
              const float* bias, const float* rscale, const float* cscale, void* stream);
 int clm_gemm_num_configs(void);
+/* the sampled search's fp16 score forms (fp16 A / W, device pointers): score = acc * rscale[m] *
+ * cscale[n] rounded toward -inf to fp16 (mode 1, out [M, ldo] u16), or the maxima of each group of
+ * 4 consecutive columns rounded the same way (mode 2, out [M, ldo >= N/4], a row's groups in a
+ * fixed permutation; config 1, N % 256 == 0) */
+int clm_gemm_scores16(int hip_device, int config, const void* A, int64_t lda, const void* W, int64_t ldw, int M,
+                      int N, int K, const float* rscale, const float* cscale, void* out, int64_t ldo, int mode,
+                      void* stream);
 /* diagnostic flags (micro-benchmarks and tests only; 0 in production), initialised from
  * $CLM_GEMM_DEBUG: for later clm_gemm calls bit 0 = skip the epilogue (accumulators kept
  * live), bit 1 = run the epilogue but drop every store, bit 2 = one tile per workgroup
@@ -238,14 +247,16 @@ void clm_debug_set(int flags);
 int clm_topk_threshold(int hip_device, const float* scores, int64_t lds, int64_t nq, int64_t C, int k,
                        float margin, int method, float* th, void* stream);
 /* attention over qkv [B*T, 3*H*64] (q pre-scaled by 64^-1/2), out [B*T, ldo] (device
- * pointers). flags: CLM_ATTN_CAUSAL (1, the text tower's mask; the argument was a 0/1 causal
- * switch and keeps that meaning), CLM_ATTN_Q_LOG2E (2): q carries log2(e) as well -- the form the
- * engine uses where the kernel takes log2-domain scores (bf16, non-causal, T > 128); CLM_E_ARG
- * for any other shape. */
-#define CLM_ATTN_CAUSAL 1
-#define CLM_ATTN_Q_LOG2E 2
+ * pointers); causal: 0 / non-0 switch (the text tower's mask). */
 int clm_attention(int hip_device, int dtype, int causal, const void* qkv, void* out, int64_t ldo,
                   int B, int T, int H, void* stream);
+/* the same with a flag word: CLM_ATTN_CAUSAL (1), CLM_ATTN_Q_LOG2E (2): q carries log2(e) as
+ * well -- the form the engine uses where the kernel takes log2-domain scores (bf16, non-causal,
+ * T > 128); CLM_E_ARG for any other shape or an unknown flag bit. */
+#define CLM_ATTN_CAUSAL 1
+#define CLM_ATTN_Q_LOG2E 2
+int clm_attention_ex(int hip_device, int dtype, int flags, const void* qkv, void* out, int64_t ldo,
+                     int B, int T, int H, void* stream);
 /* LayerNorm of fp32 rows src [M, lds] over d columns (d a multiple of 128, <= 1024), eps, fp32
  * gamma / beta -> y [M, ldy] in dtype CLM_BF16|CLM_F16 (device pointers); the encoder's kernel
  * (TF/models/clip/modeling_clip.py:358,360 nn.LayerNorm) */

@@ -188,12 +188,50 @@ def test_attention_q_log2e_vs_torch(B, T, H, ramp):
     ref_in = folded.float()   # the reference sees the same rounded q (log2 e divided back out in fp32)
     ref_in[:, : H * 64] /= 1.4426950408889634
     out = torch.full((B * T, H * 64 + 64), 7.0, device="cuda").to(torch.bfloat16)
-    C.check(C.lib().clm_attention(0, C.CLM_BF16, C.CLM_ATTN_Q_LOG2E, C.ptr(folded), C.ptr(out), out.stride(0), B, T,
-                                  H, C.stream_of(qkv.device)), "clm_attention")
+    C.check(C.lib().clm_attention_ex(0, C.CLM_BF16, C.CLM_ATTN_Q_LOG2E, C.ptr(folded), C.ptr(out), out.stride(0), B,
+                                     T, H, C.stream_of(qkv.device)), "clm_attention_ex")
     ref = _attn_ref(ref_in, B, T, H, False)
     err = (out[:, : H * 64].float() - ref).abs().max().item()
     assert err < 3e-2, err
     assert (out[:, H * 64:].float() == 7.0).all()
+
+
+@pytest.mark.parametrize("folded", [True, False])
+def test_attention_very_negative_first_tile(folded):
+    """every query's logits against the first 32 keys are ~-190 (log2 domain ~-275, below the
+    -128 where exp2(-shift) overflows): the first step's rescale must not turn the zero O and sum
+    into NaN (the log2e-folded form started its shift at 0)"""
+    B, T, H = 1, 577, 2
+    g = torch.Generator(device="cuda").manual_seed(11)
+    qkv = torch.randn((B * T, 3 * H * 64), generator=g, device="cuda") * 0.3
+    qkv[:, : H * 64] = 1.0                      # q: every dim 1
+    qkv[:32, H * 64: 2 * H * 64] = -3.0         # first 32 keys: q . k = -192 for every query
+    q_in = qkv.clone()
+    if folded:
+        q_in[:, : H * 64] *= 1.4426950408889634
+    q_in = q_in.to(torch.bfloat16)
+    ref_in = q_in.float()
+    if folded:
+        ref_in[:, : H * 64] /= 1.4426950408889634
+    out = torch.zeros((B * T, H * 64), device="cuda", dtype=torch.bfloat16)
+    C.check(C.lib().clm_attention_ex(0, C.CLM_BF16, C.CLM_ATTN_Q_LOG2E if folded else 0, C.ptr(q_in), C.ptr(out),
+                                     out.stride(0), B, T, H, C.stream_of(qkv.device)), "clm_attention_ex")
+    assert torch.isfinite(out.float()).all()
+    err = (out.float() - _attn_ref(ref_in, B, T, H, False)).abs().max().item()
+    assert err < 3e-2, err
+
+
+def test_attention_causal_switch_keeps_meaning():
+    """clm_attention's `causal` is a 0 / non-0 switch: 5 means causal, like 1"""
+    B, T, H = 2, 77, 2
+    g = torch.Generator(device="cuda").manual_seed(5)
+    qkv = torch.randn((B * T, 3 * H * 64), generator=g, device="cuda").to(torch.float16)
+    o1 = torch.zeros((B * T, H * 64), device="cuda", dtype=torch.float16)
+    o5 = torch.ones_like(o1)
+    for c, o in ((1, o1), (5, o5)):
+        C.check(C.lib().clm_attention(0, C.CLM_F16, c, C.ptr(qkv), C.ptr(o), o.stride(0), B, T, H,
+                                      C.stream_of(qkv.device)), "clm_attention")
+    assert torch.equal(o1, o5)
 
 
 @pytest.mark.parametrize("dtype,flags,T", [("float16", 2, 577), ("bfloat16", 3, 577), ("bfloat16", 2, 128),
@@ -202,7 +240,7 @@ def test_attention_q_log2e_refused(dtype, flags, T):
     """the log2(e) form exists only for the bf16, non-causal, T > 128 kernel; unknown flags refused"""
     qkv = torch.zeros((T, 3 * 64), dtype=DT[dtype][0], device="cuda")
     out = torch.zeros((T, 64), dtype=DT[dtype][0], device="cuda")
-    rc = C.lib().clm_attention(0, DT[dtype][1], flags, C.ptr(qkv), C.ptr(out), 64, 1, T, 1, C.stream_of(qkv.device))
+    rc = C.lib().clm_attention_ex(0, DT[dtype][1], flags, C.ptr(qkv), C.ptr(out), 64, 1, T, 1, C.stream_of(qkv.device))
     assert rc == C.CLM_E_ARG
 
 

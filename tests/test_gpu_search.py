@@ -113,7 +113,9 @@ def test_all_paths_agree_bit_for_bit(monkeypatch):
         for kv in PATHS[path]:
             monkeypatch.delenv(kv)
     st = idx.stats()
-    assert st["full_exact"] == nq and st["scan_bounded"] == nq and st["filtered"] == nq
+    # every query on its intended path; on failure the message carries every path counter (a
+    # round-5 scratch run once saw 7 of 40 sampled queries overflow here)
+    assert st["full_exact"] == nq and st["scan_bounded"] == nq and st["filtered"] == nq, st
     for path in ("bounded_scan", "bounded"):
         assert torch.equal(res[path][1], res["full"][1]), path
         assert torch.equal(res[path][0], res["full"][0]), path
@@ -773,3 +775,153 @@ def test_filter_tile_per_block_near_duplicates(monkeypatch):
     for (s, i), (rs, ri) in zip(runs, [ref_d, ref_d, ref_r, ref_d]):
         assert torch.equal(i, ri) and torch.equal(s, rs)
     idx.close()
+
+
+@pytest.mark.parametrize("M,N", [(512, 256 * 300), (300, 256 * 257)])
+def test_sample_group_maxima_many_tiles_per_workgroup(M, N):
+    """The sampled search's group-maxima score form (GemmArgs::out16 == 2, config 1) with more tiles
+    than workgroups, so every workgroup's LDS ring crosses tile ends after those epilogues (ADVICE
+    r05: the counted wait at a tile end must not assume more stores than this form issues). Each
+    row's stored values equal, as a multiset, f16_down of the maxima of its groups of 4 columns
+    of the fp32 scores of the same tile config; and mode 1 equals f16_down of every score."""
+    from test_host import _f16_down
+    from clip_lora_match_amd import _capi as C
+    g = torch.Generator(device="cuda").manual_seed(M + N)
+    K = 512
+    A = (torch.randn((M, K), generator=g, device="cuda") * 0.05).half()
+    W = (torch.randn((N, K), generator=g, device="cuda") * 0.05).half()
+    rs = torch.rand(M, generator=g, device="cuda") + 0.5
+    cs = torch.rand(N, generator=g, device="cuda") + 0.5
+    st = C.stream_of(A.device)
+    f32 = torch.empty((M, N), device="cuda")
+    C.check(C.lib().clm_gemm(0, C.CLM_F16, C.CLM_EPI_SCORE, 1, C.ptr(A), K, C.ptr(W), K, M, N, K, C.ptr(f32), N,
+                             None, C.ptr(rs), C.ptr(cs), st), "clm_gemm")
+    s16 = torch.empty((M, N), device="cuda", dtype=torch.int16)
+    C.check(C.lib().clm_gemm_scores16(0, 1, C.ptr(A), K, C.ptr(W), K, M, N, K, C.ptr(rs), C.ptr(cs), C.ptr(s16), N, 1,
+                                      st), "clm_gemm_scores16 mode 1")
+    ldg = N // 4 + 64
+    grp = torch.full((M, ldg), -1, device="cuda", dtype=torch.int16)
+    C.check(C.lib().clm_gemm_scores16(0, 1, C.ptr(A), K, C.ptr(W), K, M, N, K, C.ptr(rs), C.ptr(cs), C.ptr(grp), ldg,
+                                      2, st), "clm_gemm_scores16 mode 2")
+    torch.cuda.synchronize()
+    sc = f32.cpu().numpy()
+    want16 = _f16_down(sc)
+    assert np.array_equal(s16.cpu().numpy().view(np.float16), want16)
+    want = np.sort(_f16_down(sc.reshape(M, N // 4, 4).max(2)).astype(np.float32), axis=1)
+    got = grp.cpu().numpy()
+    assert (got[:, N // 4:] == -1).all()   # nothing past the row's groups
+    got = np.sort(got[:, : N // 4].view(np.float16).astype(np.float32), axis=1)
+    assert np.array_equal(got, want)
+
+
+def _set_env(monkeypatch, env):
+    for name in ("CLM_SEARCH_SMALLQ", "CLM_SEARCH_FULL", "CLM_SEARCH_BOUNDED", "CLM_SEARCH_EXACT"):
+        monkeypatch.delenv(name, raising=False)
+    for kv in env.items():
+        monkeypatch.setenv(*kv)
+
+
+@pytest.mark.parametrize("nq", [1, 2, 7, 16])
+@pytest.mark.parametrize("name", ["gauss", "clus", "gauss_f16"])
+def test_small_batch_vs_reference_golden(name, nq, monkeypatch):
+    """Small query batches -- the reference's own one-query-per-call pattern (search.py:93-99,
+    seeker_service.py:183-186) -- through the one-pass streaming search (search_small, forced at
+    this size by CLM_SEARCH_SMALLQ=1), against the reference's top_k_similar goldens: indices
+    equal up to 2e-6 near-ties, scores within 1e-6. The clustered set keeps each query's 64
+    near rows inside one 256-row chunk, so the chunk-maximum threshold is loose there and lists
+    overflow into the whole-list pass: that path is checked too. k = 50 needs 50 chunks (the
+    4,096-row index has 16) and falls back to the regular routing."""
+    _set_env(monkeypatch, {"CLM_SEARCH_SMALLQ": "1"})
+    if name == "gauss_f16":
+        g = golden("search_gauss.npz")
+        rows = syn.gaussian_rows(int(g["n"]), int(g["dim"]), int(g["row_seed"]))
+        qs = syn.gaussian_rows(int(g["nq"]), int(g["dim"]), int(g["q_seed"]))
+        key = ""
+    else:
+        g = golden("search_fp32.npz")
+        gr, gq, cr, cq = syn.fp32_search_inputs()
+        rows, qs = (gr, gq) if name == "gauss" else (cr, cq)
+        key = name + "_"
+    idx = CosineIndex(512, capacity=rows.shape[0])
+    idx.append(torch.from_numpy(rows))
+    exact = S.cosine_scores(qs.astype(np.float64), rows.astype(np.float64))
+    for k in (1, 5, 10, 50):
+        for q0 in range(0, qs.shape[0], nq):
+            s, i = idx.search(torch.from_numpy(qs[q0:q0 + nq]), k)
+            s, i = s.cpu().numpy(), i.cpu().numpy()
+            _agree(i, g[f"{key}idx_k{k}"][q0:q0 + nq], exact[q0:q0 + nq])
+            assert np.max(np.abs(s - g[f"{key}vals_k{k}"][q0:q0 + nq])) < 1e-6, (k, q0)
+    st = idx.stats()   # k = 1, 5, 10: every query on the streaming search (or its overflow pass); k = 50: the full scan
+    assert st["small_scan"] + st["overflow"] == 3 * qs.shape[0] and st["full_exact"] == qs.shape[0], st
+    assert st["small_scan"] > 0, st
+
+
+@pytest.mark.parametrize("dim,n,fp32_rows", [(512, 1_200_003, True), (768, 300_001, False), (64, 100_000, False)])
+def test_small_batch_bit_identical_to_full_scan(dim, n, fp32_rows, monkeypatch):
+    """search_small == the full exact scan, indices and scores bit for bit: nq 1 / 5 / 16, k up to
+    100, near-duplicate queries, a ragged last block and chunk (n % 256 != 0), fp32 rows (re-score
+    against the fp32 copy) and fp16-only indexes, row widths 64 / 512 / 768."""
+    g = torch.Generator(device="cuda").manual_seed(dim + n)
+    rows = torch.randn((n, dim), generator=g, device="cuda")
+    if not fp32_rows:
+        rows = rows.half()
+    q = torch.randn((16, dim), generator=g, device="cuda")
+    q[:4] = rows[torch.arange(4, device="cuda") * 1000 + 7].float() + 0.01 * q[:4]
+    q[4] = rows[n - 1].float()                      # the last (ragged) block's last row
+    idx = CosineIndex(dim, capacity=n)
+    idx.append(rows)
+    for nq in (1, 5, 16):
+        for k in (1, 5, 12, 100):
+            _set_env(monkeypatch, {"CLM_SEARCH_SMALLQ": "1"})
+            s1, i1 = idx.search(q[:nq], k)
+            _set_env(monkeypatch, {"CLM_SEARCH_FULL": "1", "CLM_SEARCH_SMALLQ": "0"})
+            s2, i2 = idx.search(q[:nq], k)
+            assert torch.equal(i1, i2) and torch.equal(s1, s2), (nq, k)
+    _set_env(monkeypatch, {})
+    assert torch.equal(i2[:4, 0], torch.arange(4, device="cuda") * 1000 + 7)
+    assert int(i2[4, 0]) == n - 1
+    st = idx.stats()
+    assert st["small_scan"] + st["overflow"] == 4 * (1 + 5 + 16) and st["small_scan"] > 0, st
+
+
+def test_small_batch_overflow_near_duplicates(monkeypatch):
+    """A query whose candidate window holds thousands of rows (5,000 near copies of one row spread
+    over many chunks, like a finder index of one description template): its list overflows
+    CAND_CAP and is rebuilt whole; the result equals the full exact scan's."""
+    n, dim = 400_000, 512
+    g = torch.Generator(device="cuda").manual_seed(3)
+    rows = torch.randn((n, dim), generator=g, device="cuda")
+    center = rows[123].clone()
+    dup = torch.arange(5000, device="cuda") * 80 + 11
+    rows[dup] = center + 1e-3 * torch.randn((5000, dim), generator=g, device="cuda")
+    idx = CosineIndex(dim, capacity=n)
+    idx.append(rows)
+    q = torch.stack([center, torch.randn(dim, generator=g, device="cuda")])
+    for k in (1, 5, 64):
+        _set_env(monkeypatch, {"CLM_SEARCH_SMALLQ": "1"})
+        s1, i1 = idx.search(q, k)
+        _set_env(monkeypatch, {"CLM_SEARCH_FULL": "1", "CLM_SEARCH_SMALLQ": "0"})
+        s2, i2 = idx.search(q, k)
+        assert torch.equal(i1, i2) and torch.equal(s1, s2), k
+    _set_env(monkeypatch, {})
+    assert idx.stats()["overflow"] >= 3, idx.stats()
+
+
+def test_small_batch_default_routing(monkeypatch):
+    """Without any switch, nq <= 16 on an index with nq * N > 2^24 takes the streaming search
+    (stats), and equals the sampled bounded search bit for bit."""
+    _set_env(monkeypatch, {})
+    n, dim = 9_000_000, 64
+    g = torch.Generator(device="cuda").manual_seed(4)
+    rows = torch.randn((n, dim), generator=g, device="cuda").half()
+    q = rows[torch.tensor([5, 8_999_999], device="cuda")].float() + 0.02 * torch.randn((2, dim), generator=g,
+                                                                                        device="cuda")
+    idx = CosineIndex(dim, capacity=n)
+    idx.append(rows)
+    s1, i1 = idx.search(q, 5)
+    assert idx.stats()["small_scan"] == 2, idx.stats()
+    _set_env(monkeypatch, {"CLM_SEARCH_SMALLQ": "0"})
+    s2, i2 = idx.search(q, 5)
+    assert idx.stats()["filtered"] == 2, idx.stats()
+    assert torch.equal(i1, i2) and torch.equal(s1, s2)
+    assert int(i1[0, 0]) == 5 and int(i1[1, 0]) == 8_999_999
