@@ -2003,7 +2003,7 @@ static int search_bounded(clm_index* x, bool sampled, int64_t S, const u16* q16,
 // search_with_embedding call (search.py:93-99, seeker_service.py:183-186). The bounded search's
 // MFMA filter pads such a batch to 256-row query tiles (>= 94 % padding) and its sampled-threshold
 // phase adds a second GEMM; here the index is streamed ONCE (scan16: fp16-pass scores of every row
-// into [nq, ldo] + each 256-row chunk's maximum), then
+// into [N, ldq], ldq = nq rounded up to a power of two, + each 256-row chunk's maximum), then
 //  1. th[q] = (k-th largest chunk maximum of q) - RESCORE_MARGIN: k chunks whose maxima are >= the
 //     k-th largest hold k distinct rows, so it is <= the fp16-pass k-th best, a lower bound like
 //     the sampled threshold (search_bounded step 1);
@@ -2012,21 +2012,26 @@ static int search_bounded(clm_index* x, bool sampled, int64_t S, const u16* q16,
 //  3. rescore_select: exact fp64 re-score and (score desc, index asc) top k -- the same routine and
 //     bits as every other path. Lists past CAND_CAP go through finish_overflow.
 // Needs nchunk >= k (N >= 256 k) and the score matrix's offsets within one buffer descriptor.
+// from this many rows on, a small batch takes search_small by default (below it the full exact
+// scan is as fast: ~1.9 ms per query per 1 M rows at 512 dims against ~0.1 ms + launches)
+constexpr int64_t SMALL_MIN_ROWS = 65536;
 static bool search_small_fits(const clm_index* x, int64_t nq, int k) {
   const int64_t N = x->n, dim = x->dim;
-  const int64_t nchunk = (N + 255) / 256, ldo = round_up(N, (int64_t)64);
+  const int64_t nchunk = (N + 255) / 256;
   return nq >= 1 && nq <= 16 && k >= 1 && k <= 1024 && dim >= 64 && dim <= 1024 && dim % 64 == 0 && nchunk >= k &&
-         (nq - 1) * ldo * 4 + 64 <= 0x7FFFFFF0LL && (nq - 1) * nchunk * 4 + 4 <= 0x7FFFFFF0LL;
+         (nq - 1) * nchunk * 4 + 4 <= 0x7FFFFFF0LL;
 }
 
 static int search_small(clm_index* x, const u16* q16, const float* qinv, const float* q32, const double* qn,
                         int64_t nq, int k, float* osc, int64_t* oix, hipStream_t st) {
   const int dim = (int)x->dim;
   const int64_t N = x->n;
-  const int64_t nchunk = (N + 255) / 256, ldo = round_up(N, (int64_t)64);
+  const int64_t nchunk = (N + 255) / 256;
+  int64_t ldq = 1;   // scores per index row, a power of two >= nq
+  while (ldq < nq) ldq *= 2;
   size_t off = 0;
   auto take = [&](size_t bytes) { size_t o = off; off = round_up(off + bytes, 256); return o; };
-  const size_t o_sc = take((size_t)nq * ldo * 4);
+  const size_t o_sc = take((size_t)N * ldq * 4);
   const size_t o_cm = take((size_t)nq * nchunk * 4);
   const size_t o_th = take((size_t)nq * 4);
   const size_t o_cnt = take((size_t)nq * 4);
@@ -2034,6 +2039,9 @@ static int search_small(clm_index* x, const u16* q16, const float* qinv, const f
   const size_t o_ti = take((size_t)nq * k * 8);
   const size_t o_cs = take((size_t)nq * CAND_CAP * 4);
   const size_t o_ci = take((size_t)nq * CAND_CAP * 8);
+  const int64_t W = scan16_waves(nchunk, dim);   // k <= 8: every wave's 8 largest chunk maxima
+  const int64_t ldw = W * 8;
+  const size_t o_wt = take((size_t)nq * ldw * 4);
   int r = grow(&x->ws2, &x->ws2_bytes, off);
   if (r) return r;
   uint8_t* w = (uint8_t*)x->ws2;
@@ -2044,16 +2052,19 @@ static int search_small(clm_index* x, const u16* q16, const float* qinv, const f
   Scan16Args a{};
   a.rows = x->rows; a.inv = x->inv; a.N = N; a.dim = dim;
   a.q16 = q16; a.qinv = qinv; a.nq = (int)nq;
-  a.out = sc; a.ldo = ldo; a.cmax = cm; a.nchunk = nchunk;
+  a.out = sc; a.ldo = ldq; a.cmax = cm; a.nchunk = nchunk;
+  const bool wave_top = k <= 8 && !g_kth_radix && W * 8 >= k;
+  a.wtop = wave_top ? (float*)(w + o_wt) : nullptr; a.ldw = ldw;
   KCHK(scan16(a, st));
-  if (k <= 8 && !g_kth_radix) {
-    KCHK(kth_thresholds(cm, nchunk, nq, nchunk, k, RESCORE_MARGIN, th, st));
+  if (wave_top) {   // the k-th largest of the waves' top-8 lists = the k-th largest chunk maximum
+    KCHK(kth_thresholds((const float*)(w + o_wt), ldw, nq, ldw, k, RESCORE_MARGIN, th, st));
   } else {
     KCHK(topk_rows(cm, nchunk, nq, nchunk, k, 0, (float*)(w + o_ts), (int64_t*)(w + o_ti), k, st));
     KCHK(filter_thresholds((const float*)(w + o_ts), k, nq, k, RESCORE_MARGIN, th, st));
   }
   HIPCHK(hipMemsetAsync(cnt, 0, (size_t)nq * 4, st));
-  KCHK(collect_ge(sc, ldo, nq, N, th, cnt, CAND_CAP, (float*)(w + o_cs), (int64_t*)(w + o_ci), x->offset, st));
+  KCHK(collect_ge(sc, (int)ldq, (int)nq, N, th, cnt, CAND_CAP, (float*)(w + o_cs), (int64_t*)(w + o_ci), x->offset,
+                  st));
   const void* xrows = x->rows32 ? (const void*)x->rows32 : (const void*)x->rows;
   KCHK(rescore_select((const float*)(w + o_cs), (const int64_t*)(w + o_ci), cnt, CAND_CAP, q32, qn, dim, xrows,
                       !x->rows32, x->offset, RESCORE_MARGIN, nq, k, osc, oix, st));
@@ -2133,7 +2144,7 @@ int clm_index_search(clm_index* x, const void* q, int q_dtype, int64_t nq, int k
   const int small_mode = e_small ? atoi(e_small) : -1;
   const bool small = small_mode != 0 && k <= 1024 && N > 0 && search_small_fits(x, nq, k) &&
                      (small_mode == 1 || (!force_bounded && !(e_full && atoi(e_full)) && !(e_exact && atoi(e_exact)) &&
-                                          (double)nq * (double)N > (double)(1 << 24)));
+                                          N >= SMALL_MIN_ROWS));
   if (small) {
     r = search_small(x, q16, qinv, q32, qn, nq, k, osc, oix, st);
   } else if (k > 1024) {

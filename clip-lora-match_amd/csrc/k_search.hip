@@ -942,10 +942,11 @@ namespace {
 //    filled by buffer_load ... lds (one 1 KiB wave-instruction per 512 row bytes, whole rows, the
 //    16-B chunks XOR-swizzled on the source so the fragment reads are conflict-free) plus one DMA of
 //    the block's 16 inverse norms. No barriers: a wave reads only the blocks it loaded;
-//  * per block, dim / 32 v_mfma_f32_16x16x32_f16 with the index rows on the A port and the (<= 16)
-//    unit-rounded fp16 queries held in registers on the B port: lane l ends with rows 4 (l >> 4) ..
-//    +3 of query l & 15, scored as the EPI_SCORE epilogue does (acc * qinv[q] * inv[row]), stored
-//    16 B per lane into the [nq, ldo] score matrix, and max-reduced into the chunk's maximum;
+//  * per block, dim / 32 v_mfma_f32_16x16x32_f16 with the (<= 16) unit-rounded fp16 queries held in
+//    registers on the A port and the index rows on the B port: lane l ends with queries 4 (l >> 4)
+//    .. +3 of row l & 15, scored as the EPI_SCORE epilogue does (acc * qinv[q] * inv[row]), stored
+//    into the row-major [N, ldq] score matrix (a block's scores one contiguous piece: 16 B per lane
+//    for ldq >= 4) and max-reduced into the chunk's maxima;
 //  * cmax[q][chunk] = the largest fp16-pass score of the chunk (NaN scores ignored, rows past N
 //    -inf). The k-th largest chunk maximum is at most the k-th largest score of the whole index
 //    (k chunks whose maxima reach it hold k distinct rows), so th = that - margin bounds the
@@ -962,7 +963,9 @@ __device__ __forceinline__ void scan16_body(const Scan16Args& a) {
   constexpr int BLK = 16 * RB + 1024;    // a block's LDS image: 16 rows, then its inverse norms
   constexpr int F0 = 1 + (D - 2) * (KS + 2);
   constexpr int F = F0 > 63 ? 63 : F0;
-  const int lane = threadIdx.x & 63, g = lane >> 4, qj = lane & 15;
+  // lane: row rr of a 16-row block (B port / C column), query group g: queries 4 g .. 4 g + 3
+  // (C rows); on the A port the lane carries query rr
+  const int lane = threadIdx.x & 63, g = lane >> 4, rr = lane & 15;
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int nw = blockDim.x >> 6;
   const int64_t W = (int64_t)gridDim.x * nw;
@@ -970,17 +973,43 @@ __device__ __forceinline__ void scan16_body(const Scan16Args& a) {
   const int64_t nchunk = a.nchunk;
   const int64_t my = w < nchunk ? (nchunk - 1 - w) / W + 1 : 0;
   const int64_t nb = my * (SCAN_CHUNK / 16);
-  if (nb == 0) return;
+  const int ldq = (int)a.ldo;   // scores per row: 1, 2, 4, 8 or 16 (>= nq)
+  // the wave's 8 largest chunk maxima of queries 4 g + u (sorted descending, every lane of the
+  // group), written at the end: the k-th largest over every wave's list is the k-th largest chunk
+  // maximum for k <= 8, without a pass over [nq, nchunk] (one workgroup per query spent 74 us on it
+  // at 10 M rows)
+  float top[4][KTH_MAX];
+#pragma unroll
+  for (int u = 0; u < 4; ++u)
+#pragma unroll
+    for (int j = 0; j < KTH_MAX; ++j) top[u][j] = -INFINITY;
+  auto write_top = [&]() {
+    const auto tb = buf_rsrc(a.wtop + w * KTH_MAX);
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int j = 0; j < KTH_MAX; ++j) {
+        const int q = 4 * g + u;
+        const uint32_t to = (rr == 0 && q < a.nq) ? (uint32_t)(((int64_t)q * a.ldw + j) * 4) : BUF_OOB;
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(top[u][j]), tb, to, 0, 0);
+      }
+  };
+  if (nb == 0) {
+    if (a.wtop) write_top();
+    return;
+  }
   uint8_t* ring = smem + wid * D * BLK;
   // chunk swizzle: 16 consecutive rows at one chunk position land on 16 distinct bank quads
   auto sw = [](int r) { return RB >= 256 ? (r & 15) : ((r >> 1) & 7); };
-  u32x4 qf[KS];   // B port: query qj, dims (4 s + g) * 8 .. + 7
+  u32x4 qf[KS];   // A port: query rr, dims (4 s + g) * 8 .. + 7
   {
-    const u16* qp = a.q16 + (int64_t)min(qj, a.nq - 1) * (KS * 32) + g * 8;
+    const u16* qp = a.q16 + (int64_t)min(rr, a.nq - 1) * (KS * 32) + g * 8;
 #pragma unroll
-    for (int s = 0; s < KS; ++s) qf[s] = qj < a.nq ? *(const u32x4*)(qp + s * 32) : u32x4{0u, 0u, 0u, 0u};
+    for (int s = 0; s < KS; ++s) qf[s] = rr < a.nq ? *(const u32x4*)(qp + s * 32) : u32x4{0u, 0u, 0u, 0u};
   }
-  const float qs = qj < a.nq ? a.qinv[qj] : 0.f;
+  float qs[4];   // inverse norms of queries 4 g + u
+#pragma unroll
+  for (int u = 0; u < 4; ++u) qs[u] = 4 * g + u < a.nq ? a.qinv[4 * g + u] : 0.f;
   uint32_t doff[KS];   // DMA: instruction t, lane -> LDS slot t * 1 KiB + 16 lane of the block image
 #pragma unroll
   for (int t = 0; t < KS; ++t) {
@@ -988,9 +1017,9 @@ __device__ __forceinline__ void scan16_body(const Scan16Args& a) {
     doff[t] = (uint32_t)(r * RB + ((p ^ sw(r)) * 16));
   }
   const uint32_t ioff = lane < 4 ? (uint32_t)lane * 16 : BUF_OOB;
-  uint32_t foff[KS];   // A port: row qj of the block, chunk 4 s + g
+  uint32_t foff[KS];   // B port: row rr of the block, chunk 4 s + g
 #pragma unroll
-  for (int s = 0; s < KS; ++s) foff[s] = (uint32_t)(qj * RB + (((4 * s + g) ^ sw(qj)) * 16));
+  for (int s = 0; s < KS; ++s) foff[s] = (uint32_t)(rr * RB + (((4 * s + g) ^ sw(rr)) * 16));
   auto row0_of = [&](int64_t i) { return (w + (i >> 4) * W) * SCAN_CHUNK + (i & 15) * 16; };
   auto issue = [&](int64_t i, int buf) {
     const int64_t r0 = row0_of(i);
@@ -1006,7 +1035,7 @@ __device__ __forceinline__ void scan16_body(const Scan16Args& a) {
 #pragma unroll
   for (int j = 0; j < D - 1; ++j)
     if (j < nb) issue(j, j);
-  float run = -INFINITY;
+  float run[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
   int buf = 0;
   for (int64_t i = 0; i < nb; ++i) {
     if (i < D - 1 || i > nb - D) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1018,37 +1047,57 @@ __device__ __forceinline__ void scan16_body(const Scan16Args& a) {
     u32x4 af[KS];
 #pragma unroll
     for (int s = 0; s < KS; ++s) af[s] = *(const u32x4*)(blk + foff[s]);
-    // the inverse norms through an asm read: the compiler's LDS-DMA alias tracking put a vmcnt(0)
-    // (every DMA in flight, the whole ring) in front of this read when it was a plain load
-    u32x4 ivr;
-    asm volatile("ds_read_b128 %0, %1" : "=v"(ivr) : "v"((uint32_t)(uintptr_t)(blk + 16 * RB + g * 16)) : "memory");
+    // the row's inverse norm through an asm read: the compiler's LDS-DMA alias tracking put a
+    // vmcnt(0) (every DMA in flight, the whole ring) in front of this read when it was a plain load
+    uint32_t ivb;
+    asm volatile("ds_read_b32 %0, %1" : "=v"(ivb) : "v"((uint32_t)(uintptr_t)(blk + 16 * RB + rr * 4)) : "memory");
     f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int s = 0; s < KS; ++s) acc = mfma16<false>(af[s], qf[s], acc);
-    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(ivr));
-    const float4 iv = make_float4(__uint_as_float(ivr[0]), __uint_as_float(ivr[1]), __uint_as_float(ivr[2]),
-                                  __uint_as_float(ivr[3]));
+    for (int s = 0; s < KS; ++s) acc = mfma16<false>(qf[s], af[s], acc);
+    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(ivb));
+    const float iv = __uint_as_float(ivb);
     const int64_t r0 = row0_of(i);
-    const int64_t rb = r0 + g * 4;   // the lane's first row
-    const float ivv[4] = {iv.x, iv.y, iv.z, iv.w};
+    const bool live = r0 + rr < a.N;
     float v[4];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) v[u] = rb + u < a.N ? acc[u] * qs * ivv[u] : -INFINITY;
-    run = fmaxf(run, fmaxf(fmaxf(v[0], v[1]), fmaxf(v[2], v[3])));
-    const auto ob = buf_rsrc(a.out + r0);
-    const uint32_t oo = (qj < a.nq && rb < a.N) ? (uint32_t)(((int64_t)qj * a.ldo + g * 4) * 4) : BUF_OOB;
-    __builtin_amdgcn_raw_buffer_store_b128(u32x4{__float_as_uint(v[0]), __float_as_uint(v[1]), __float_as_uint(v[2]),
-                                                 __float_as_uint(v[3])}, ob, oo, 0, 0);
-    if ((i & 15) == 15) {   // chunk end: its maximum per query (lanes l, l ^ 16, l ^ 32, l ^ 48)
-      const float m = cross_rows_reduce<true>(run);
+    for (int u = 0; u < 4; ++u) {
+      v[u] = live ? acc[u] * qs[u] * iv : -INFINITY;
+      run[u] = fmaxf(run[u], v[u]);
+    }
+    // scores [N, ldq], the row's queries contiguous: a block's 16 rows are one contiguous piece
+    const auto ob = buf_rsrc(a.out + r0 * ldq);
+    if (ldq >= 4) {
+      const uint32_t oo = (live && 4 * g < a.nq) ? (uint32_t)((rr * ldq + 4 * g) * 4) : BUF_OOB;
+      __builtin_amdgcn_raw_buffer_store_b128(u32x4{__float_as_uint(v[0]), __float_as_uint(v[1]),
+                                                   __float_as_uint(v[2]), __float_as_uint(v[3])}, ob, oo, 0, 0);
+    } else if (ldq == 2) {
+      const uint32_t oo = (live && g == 0) ? (uint32_t)(rr * 8) : BUF_OOB;
+      __builtin_amdgcn_raw_buffer_store_b64(u32x2{__float_as_uint(v[0]), __float_as_uint(v[1])}, ob, oo, 0, 0);
+    } else {
+      const uint32_t oo = (live && g == 0) ? (uint32_t)(rr * 4) : BUF_OOB;
+      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v[0]), ob, oo, 0, 0);
+    }
+    if ((i & 15) == 15) {   // chunk end: its maximum per query (the 16 row lanes of each group)
       const int64_t chunk = w + (i >> 4) * W;
       const auto cb = buf_rsrc(a.cmax + chunk);
-      const uint32_t co = (g == 0 && qj < a.nq) ? (uint32_t)((int64_t)qj * nchunk * 4) : BUF_OOB;
-      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(m), cb, co, 0, 0);
-      run = -INFINITY;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const float m = group16_max(run[u]);
+        run[u] = -INFINITY;
+        const int q = 4 * g + u;
+        const uint32_t co = (rr == 0 && q < a.nq) ? (uint32_t)((int64_t)q * nchunk * 4) : BUF_OOB;
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(m), cb, co, 0, 0);
+        if (m > top[u][KTH_MAX - 1]) {   // never NaN: fmaxf dropped NaN scores
+          top[u][KTH_MAX - 1] = m;
+#pragma unroll
+          for (int j = KTH_MAX - 1; j > 0; --j)
+            if (top[u][j] > top[u][j - 1]) { const float t = top[u][j]; top[u][j] = top[u][j - 1]; top[u][j - 1] = t; }
+        }
+      }
     }
     buf = buf + 1 == D ? 0 : buf + 1;
   }
+  if (a.wtop) write_top();
 }
 
 // (the body lives in a __device__ function: written inline in the kernel, hipcc's host pass left
@@ -1058,30 +1107,50 @@ __global__ __launch_bounds__(256, 1) void scan16_kernel(Scan16Args a) {
   scan16_body<KS, D>(a);
 }
 
-// candidates of the small-batch search: every (score, global row) of row q of S [nq, lds] at or
-// above th[q], appended to q's list (capacity cap; cnt[q] counts them all, so cnt > cap marks an
-// overflow). The list order is the atomics' (rescore_select sorts by (score, index)).
-__global__ __launch_bounds__(256) void collect_ge_kernel(const float* S, int64_t lds, int64_t C, const float* th,
+// candidates of the small-batch search: every (score, global row) of the score matrix S [C rows,
+// ldq] (ldq a power of two >= nq; query q in column q) at or above th[q], appended to q's list
+// (capacity cap; cnt[q] counts them all, so cnt > cap marks an overflow). The list order is the
+// atomics' (rescore_select sorts by (score, index)).
+__global__ __launch_bounds__(256) void collect_ge_kernel(const float* S, int lq, int nq, int64_t C, const float* th,
                                                          int* cnt, int cap, float* cs, int64_t* ci, int64_t base) {
-  const int64_t q = blockIdx.y;
-  const float t = th[q];
-  const float* s = S + q * lds;
-  for (int64_t j4 = (int64_t)blockIdx.x * 256 + threadIdx.x; j4 * 4 < C; j4 += (int64_t)gridDim.x * 256) {
-    const float4 v4 = *(const float4*)(s + j4 * 4);
-    const float v[4] = {v4.x, v4.y, v4.z, v4.w};
+  const int ldq = 1 << lq;
+  float t[16];
+#pragma unroll
+  for (int q = 0; q < 16; ++q) t[q] = q < nq ? th[q] : INFINITY;
+  const int64_t n4 = ((C << lq) + 3) >> 2;   // float4 groups, the last one possibly partial
+  for (int64_t e4 = (int64_t)blockIdx.x * 256 + threadIdx.x; e4 < n4; e4 += (int64_t)gridDim.x * 256) {
+    float v[4];
+    const int64_t e0 = e4 * 4;
+    if (e0 + 4 <= (C << lq)) {
+      const float4 x = *(const float4*)(S + e0);
+      v[0] = x.x; v[1] = x.y; v[2] = x.z; v[3] = x.w;
+    } else {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) v[u] = e0 + u < (C << lq) ? S[e0 + u] : -INFINITY;
+    }
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
-      const int64_t j = j4 * 4 + u;
-      if (j < C && v[u] >= t) {
+      const int64_t e = e0 + u;
+      const int q = (int)(e & (ldq - 1));
+      float tq = t[0];
+#pragma unroll
+      for (int j = 1; j < 16; ++j) tq = q == j ? t[j] : tq;
+      if (v[u] >= tq && q < nq) {
         const int slot = atomicAdd(cnt + q, 1);
         if (slot < cap) {
-          cs[q * cap + slot] = v[u];
-          ci[q * cap + slot] = base + j;
+          cs[(int64_t)q * cap + slot] = v[u];
+          ci[(int64_t)q * cap + slot] = base + (e >> lq);
         }
       }
     }
   }
 }
+
+}  // namespace
+int scan16_grid(int64_t nchunk, int nw, int cus) {
+  return (int)std::max<int64_t>(1, std::min<int64_t>(cus, (nchunk + nw - 1) / nw));
+}
+namespace {
 
 template <int KS, int D>
 hipError_t scan16_launch(const Scan16Args& a, int nw, hipStream_t st) {
@@ -1101,8 +1170,8 @@ hipError_t scan16_launch(const Scan16Args& a, int nw, hipStream_t st) {
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1) cus = 256;
     (void)hipGetLastError();
   }
-  const int64_t waves_needed = a.nchunk;
-  const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(cus, (waves_needed + nw - 1) / nw));
+  const int grid = scan16_grid(a.nchunk, nw, cus);
+  if ((int64_t)grid * nw * KTH_MAX > a.ldw && a.wtop) return hipErrorInvalidValue;
   kern<<<dim3(grid), dim3(nw * 64), lds, st>>>(a);
   return hipGetLastError();
 }
@@ -1118,27 +1187,37 @@ hipError_t scan16_depth(const Scan16Args& a, int nw, int depth, hipStream_t st) 
 }
 }  // namespace
 
-// waves per workgroup and ring depth for a row width: the most blocks in flight per CU that the
-// 160 KiB of LDS holds (NW x (D - 1)), fewer waves first on a tie; $CLM_SCAN_NW / $CLM_SCAN_D (A/B)
+// waves per workgroup and ring depth for a row width: one wave per CU with the deepest ring the
+// LDS and the 6-bit vmcnt hold (4 blocks: 3 in flight, 51 KiB at 512 dims) -- at 10 M x 512 that
+// streamed 1.83 ms per query against 1.87-1.93 for 2-4 waves with 2-4 blocks each
+// (profiles/r06_v1_scan16_shape_ab.txt: the many-wave forms split the 39 k chunks less evenly);
+// $CLM_SCAN_NW / $CLM_SCAN_D (A/B)
 void scan16_shape(int dim, int* nw, int* depth) {
   const int blk = 16 * dim * 2 + 1024;
   static const int env_nw = getenv("CLM_SCAN_NW") ? atoi(getenv("CLM_SCAN_NW")) : 0;
   static const int env_d = getenv("CLM_SCAN_D") ? atoi(getenv("CLM_SCAN_D")) : 0;
-  int best_w = 0, best_d = 0, best = -1;
-  for (int d = 2; d <= 4; ++d)
-    for (int w = 1; w <= 4; ++w) {
-      if ((env_nw && w != env_nw) || (env_d && d != env_d) || w * d * blk > 160 * 1024) continue;
-      const int f = w * (d - 1);
-      if (f > best) { best = f; best_w = w; best_d = d; }
-    }
-  *nw = best_w;
-  *depth = best_d;
+  int w = env_nw > 0 ? std::min(env_nw, 4) : 1;
+  int d = env_d > 0 ? std::min(std::max(env_d, 2), 4) : 4;
+  while (d > 2 && w * d * blk > 160 * 1024) --d;
+  while (w > 1 && w * d * blk > 160 * 1024) --w;
+  *nw = w * d * blk <= 160 * 1024 ? w : 0;
+  *depth = d;
+}
+
+int64_t scan16_waves(int64_t nchunk, int dim) {
+  int nw = 0, d = 0;
+  scan16_shape(dim, &nw, &d);
+  int dev = 0, cus = 0;
+  (void)hipGetDevice(&dev);
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1) cus = 256;
+  (void)hipGetLastError();
+  return (int64_t)scan16_grid(nchunk, std::max(nw, 1), cus) * std::max(nw, 1);
 }
 
 hipError_t scan16(const Scan16Args& a, hipStream_t st) {
   if (a.N <= 0 || a.nq <= 0) return hipSuccess;
-  if (a.nq > 16 || a.dim % 64 || a.dim < 64 || a.dim > 1024 || a.ldo % 4 || a.ldo < a.N ||
-      (int64_t)(a.nq - 1) * a.ldo * 4 + 64 > 0x7FFFFFF0 || (int64_t)(a.nq - 1) * a.nchunk * 4 + 4 > 0x7FFFFFF0 ||
+  if (a.nq > 16 || a.dim % 64 || a.dim < 64 || a.dim > 1024 || a.ldo < a.nq || a.ldo > 16 ||
+      (a.ldo & (a.ldo - 1)) || (int64_t)(a.nq - 1) * a.nchunk * 4 + 4 > 0x7FFFFFF0 ||
       a.nchunk != (a.N + SCAN_CHUNK - 1) / SCAN_CHUNK)
     return hipErrorInvalidValue;
   int nw = 0, d = 0;
@@ -1165,13 +1244,15 @@ hipError_t scan16(const Scan16Args& a, hipStream_t st) {
   }
 }
 
-hipError_t collect_ge(const float* scores, int64_t lds, int64_t nq, int64_t C, const float* th, int* cnt, int cap,
-                      float* cs, int64_t* ci, int64_t base, hipStream_t s) {
+hipError_t collect_ge(const float* scores, int ldq, int nq, int64_t C, const float* th, int* cnt, int cap, float* cs,
+                      int64_t* ci, int64_t base, hipStream_t s) {
   if (nq <= 0 || C <= 0) return hipSuccess;
-  if ((lds & 3) || ((uintptr_t)scores & 15) || nq > 65535) return hipErrorInvalidValue;
-  const int64_t n4 = (C + 3) / 4;
-  const unsigned gx = (unsigned)std::max<int64_t>(1, std::min<int64_t>((n4 + 255) / 256, 2048));
-  collect_ge_kernel<<<dim3(gx, (unsigned)nq), 256, 0, s>>>(scores, lds, C, th, cnt, cap, cs, ci, base);
+  int lq = 0;
+  while ((1 << lq) < ldq) ++lq;
+  if ((1 << lq) != ldq || ldq > 16 || nq > ldq || ((uintptr_t)scores & 15)) return hipErrorInvalidValue;
+  const int64_t n4 = ((C << lq) + 3) / 4;
+  const unsigned gx = (unsigned)std::max<int64_t>(1, std::min<int64_t>((n4 + 255) / 256, 4096));
+  collect_ge_kernel<<<gx, 256, 0, s>>>(scores, lq, nq, C, th, cnt, cap, cs, ci, base);
   return hipGetLastError();
 }
 

@@ -236,21 +236,26 @@ hipError_t kth_thresholds(const float* scores, int64_t lds, int64_t nq, int64_t 
 hipError_t value_bounds(const float* v, int64_t n, unsigned* keys, hipStream_t s);
 // small-batch search scan (k_search.hip scan16_kernel): nq <= 16 unit-rounded fp16 queries q16
 // [nq, dim] (inverse norms qinv) against the fp16 index rows [N, dim] (inverse norms inv), one
-// streaming pass: out [nq, ldo] = fp16-pass scores (acc * qinv * inv, -inf past N inside ldo),
-// cmax [nq, nchunk] = each 256-row chunk's largest score (nchunk = ceil(N / 256));
-// dim % 64 == 0, 64 <= dim <= 1024
+// streaming pass: out [N, ldo] = fp16-pass scores (acc * qinv * inv), row-major with the queries
+// of a row contiguous (ldo = 1, 2, 4, 8 or 16 >= nq), cmax [nq, nchunk] = each 256-row chunk's
+// largest score (nchunk = ceil(N / 256)); dim % 64 == 0, 64 <= dim <= 1024
+// wtop (optional) [nq, ldw]: wave w's 8 largest chunk maxima per query at columns 8 w .. 8 w + 7
+// (-inf padded); scan16_waves gives the wave count W (ldw >= 8 W)
 struct Scan16Args {
   const u16* rows; const float* inv; int64_t N; int dim;
   const u16* q16; const float* qinv; int nq;
   float* out; int64_t ldo;
   float* cmax; int64_t nchunk;
+  float* wtop; int64_t ldw;
 };
 hipError_t scan16(const Scan16Args& a, hipStream_t s);
 void scan16_shape(int dim, int* nw, int* depth);
-// append every (score, base + column) of row q of scores [nq, lds] (C columns) at or above th[q]
-// to q's candidate list [cap] (cnt[q] counts them all)
-hipError_t collect_ge(const float* scores, int64_t lds, int64_t nq, int64_t C, const float* th, int* cnt, int cap,
-                      float* cs, int64_t* ci, int64_t base, hipStream_t s);
+int scan16_grid(int64_t nchunk, int nw, int cus);
+int64_t scan16_waves(int64_t nchunk, int dim);
+// append every (score, base + row) of column q of scores [C rows, ldq] (ldq a power of two, 1..16,
+// >= nq) at or above th[q] to q's candidate list [cap] (cnt[q] counts them all)
+hipError_t collect_ge(const float* scores, int ldq, int nq, int64_t C, const float* th, int* cnt, int cap, float* cs,
+                      int64_t* ci, int64_t base, hipStream_t s);
 __host__ __device__ inline unsigned float_key(float f) {
   const unsigned b = __builtin_bit_cast(unsigned, f);
   return (b & 0x80000000u) ? ~b : (b | 0x80000000u);

@@ -908,8 +908,9 @@ def test_small_batch_overflow_near_duplicates(monkeypatch):
 
 
 def test_small_batch_default_routing(monkeypatch):
-    """Without any switch, nq <= 16 on an index with nq * N > 2^24 takes the streaming search
-    (stats), and equals the sampled bounded search bit for bit."""
+    """Without any switch, nq <= 16 on an index of >= 65,536 rows takes the streaming search
+    (stats), and equals the sampled bounded search bit for bit; one query per call too (the
+    reference's pattern, which the full exact scan served before round 6)."""
     _set_env(monkeypatch, {})
     n, dim = 9_000_000, 64
     g = torch.Generator(device="cuda").manual_seed(4)
@@ -925,3 +926,7 @@ def test_small_batch_default_routing(monkeypatch):
     assert idx.stats()["filtered"] == 2, idx.stats()
     assert torch.equal(i1, i2) and torch.equal(s1, s2)
     assert int(i1[0, 0]) == 5 and int(i1[1, 0]) == 8_999_999
+    _set_env(monkeypatch, {})
+    s3, i3 = idx.search(q[1], 5)
+    assert idx.stats()["small_scan"] == 3, idx.stats()
+    assert torch.equal(i3[0], i1[1]) and torch.equal(s3[0], s1[1])
