@@ -554,8 +554,10 @@ def encode_item_leg(device, dtype: str, calls: int = 32) -> dict:
             yaml.safe_dump({"model": {"name": "openai/clip-vit-base-patch32", "device": "cuda",
                                       "tokenizer_dir": os.path.join(REPO, "tests", "golden", "clip_bpe")},
                             "preprocess": {"image_size": 224}}, f)
-        model, proc, dv = load_clip_model(cfgp, use_lora=True, lora_weights_path="synthetic",
-                                          weights_dir="synthetic", max_batch=1, compute_dtype=dtype)
+        import contextlib
+        with contextlib.redirect_stdout(sys.stderr):   # the loader's progress prints: stdout is the JSON line
+            model, proc, dv = load_clip_model(cfgp, use_lora=True, lora_weights_path="synthetic",
+                                              weights_dir="synthetic", max_batch=1, compute_dtype=dtype)
         paths = []
         for i in range(4):
             p = os.path.join(d, f"item{i}.jpg")
