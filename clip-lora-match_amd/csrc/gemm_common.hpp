@@ -445,4 +445,7 @@ constexpr int epi_min_stores() {
 
 // G2 kernels (k_gemm2.hip): configs 8-11
 hipError_t gemm2_launch(bool bf16, int epi, int id, const GemmArgs& g, hipStream_t s);
+// G4 kernels (k_gemm4.hip): configs 13 (256 x 256) / 14 (256 x 128), 4 waves of 128 x BN/2
+bool gemm4_supports(int epi, const GemmArgs& g);
+hipError_t gemm4_launch(bool bf16, int epi, int id, const GemmArgs& g, hipStream_t s);
 }  // namespace clm

@@ -270,11 +270,12 @@ hipError_t launch_id(int id, const GemmArgs& g, hipStream_t s) {
     case 7: return launch_cfg<BF, EPI, 160, 128, 2, 2, 2>(g, s);
     case 8: case 9: case 10: case 11: return gemm2_launch(BF, EPI, id, g, s);
     case 12: return launch_cfg<BF, EPI, 64, 64, 4, 1, 3>(g, s);
+    case 13: case 14: return gemm4_launch(BF, EPI, id, g, s);
     default: return hipErrorInvalidValue;
   }
 }
 
-constexpr int NCFG = 13;
+constexpr int NCFG = 15;
 static_assert(GEMM_CFG_SKINNY == 12, "config 12 is the 64 x 64 tile");
 static_assert(GEMM_CFG_SPLITK == 2, "config 2 is the 128 x 64 tile");
 
@@ -371,6 +372,11 @@ hipError_t gemm_cfg(bool bf16, int epi, int config, const GemmArgs& g, hipStream
       if (config >= 0) return hipErrorInvalidValue;
       id = pick_from(MODELS, g.M, g.N);
     }
+  }
+  // G4 (configs 13 / 14): STORE / GELU (N, ldo multiples of 8) / RESID (of 4), whole K-steps
+  if (id >= 13 && !gemm4_supports(epi, g)) {
+    if (config >= 0) return hipErrorInvalidValue;
+    id = pick_from(MODELS, g.M, g.N);
   }
   return bf16 ? dispatch<true>(epi, id, g, s) : dispatch<false>(epi, id, g, s);
 }

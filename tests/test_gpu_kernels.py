@@ -20,8 +20,20 @@ def _gemm(dtype, epi, cfg, A, W, out, bias=None, rs=None, cs=None):
                              C.stream_of(A.device)), "clm_gemm")
 
 
+def _g4_ok(cfg, epi, N, K, ldo):
+    """configs 13 / 14 (G4, k_gemm4.hip gemm4_supports): STORE / GELU with N, ldo multiples of 8,
+    RESID with multiples of 4, whole 64-deep K-steps; anything else is refused (CLM_E_HIP)"""
+    if cfg < 13:
+        return True
+    if K % 64 or N % 4 or ldo % 4:
+        return False
+    if epi == C.CLM_EPI_RESID:
+        return True
+    return epi in (C.CLM_EPI_STORE, C.CLM_EPI_GELU) and N % 8 == 0 and ldo % 8 == 0
+
+
 @pytest.mark.parametrize("dtype", ["bfloat16", "float16"])
-@pytest.mark.parametrize("cfg", list(range(13)) + [-1])
+@pytest.mark.parametrize("cfg", list(range(15)) + [-1])
 @pytest.mark.parametrize("shape", [(333, 200, 128), (1000, 768, 768), (77, 2304, 512), (97, 100, 64), (65, 50, 128),
                                    (300, 136, 800), (257, 64, 544)])
 def test_gemm_epilogues_vs_torch(dtype, cfg, shape):
@@ -40,22 +52,31 @@ def test_gemm_epilogues_vs_torch(dtype, cfg, shape):
         with pytest.raises(Exception):
             _gemm(dtype, C.CLM_EPI_STORE, cfg, A, W, out, bias)
         return
-    _gemm(dtype, C.CLM_EPI_STORE, cfg, A, W, out, bias)
     tol = 2e-2 if dtype == "bfloat16" else 4e-3
-    assert (out.float() - ref).abs().max() <= tol * ref.abs().max()
-    _gemm(dtype, C.CLM_EPI_GELU, cfg, A, W, out, bias)
+
+    def run(epi, o, *a):
+        if not _g4_ok(cfg, epi, N, K, o.stride(0)):
+            with pytest.raises(Exception):
+                _gemm(dtype, epi, cfg, A, W, o, *a)
+            return False
+        _gemm(dtype, epi, cfg, A, W, o, *a)
+        return True
+
+    if run(C.CLM_EPI_STORE, out, bias):
+        assert (out.float() - ref).abs().max() <= tol * ref.abs().max()
     refg = ref * torch.sigmoid(1.702 * ref)
-    assert (out.float() - refg).abs().max() <= tol * refg.abs().max()
+    if run(C.CLM_EPI_GELU, out, bias):
+        assert (out.float() - refg).abs().max() <= tol * refg.abs().max()
     h = torch.randn((M, N), generator=g, device="cuda")
     h0 = h.clone()
-    _gemm(dtype, C.CLM_EPI_RESID, cfg, A, W, h, bias)
-    assert (h - (h0 + ref)).abs().max() <= 1e-3 * ref.abs().max() + 1e-5
+    if run(C.CLM_EPI_RESID, h, bias):
+        assert (h - (h0 + ref)).abs().max() <= 1e-3 * ref.abs().max() + 1e-5
     rs = torch.rand(M, generator=g, device="cuda") + 0.5
     cs = torch.rand(N, generator=g, device="cuda") + 0.5
     sc = torch.empty((M, N), dtype=torch.float32, device="cuda")
-    _gemm(dtype, C.CLM_EPI_SCORE, cfg, A, W, sc, None, rs, cs)
-    refs = (A.float() @ W.float().T) * rs[:, None] * cs[None, :]
-    assert (sc - refs).abs().max() <= 1e-4 * refs.abs().max() + 1e-6
+    if run(C.CLM_EPI_SCORE, sc, None, rs, cs):
+        refs = (A.float() @ W.float().T) * rs[:, None] * cs[None, :]
+        assert (sc - refs).abs().max() <= 1e-4 * refs.abs().max() + 1e-6
 
 
 @pytest.mark.parametrize("epi", ["STORE", "GELU", "RESID", "SCORE"])
@@ -76,6 +97,8 @@ def test_gemm_row_invariance_and_bounds(epi, N):
     init = torch.randn((M + 40, ldo), generator=g, device="cuda").to(odt)
     ref = None
     for cfg in list(range(C.lib().clm_gemm_num_configs())) + [-1]:
+        if not _g4_ok(cfg, code, N, K, ldo):
+            continue
         out = init.clone()
         _gemm(dtype, code, cfg, A, W, out[:M], bias, rs, cs)
         assert torch.equal(out[:, N:], init[:, N:]) and torch.equal(out[M:], init[M:]), f"cfg {cfg} wrote outside"
@@ -88,7 +111,7 @@ def test_gemm_row_invariance_and_bounds(epi, N):
         assert torch.equal(out, ref), f"cfg {cfg} differs from cfg 0"
 
 
-@pytest.mark.parametrize("shape", [(8200, 2100, 64), (8200, 2100, 192), (8200, 2098, 128)])
+@pytest.mark.parametrize("shape", [(8200, 2100, 64), (8200, 2100, 192), (8200, 2098, 128), (8200, 2112, 320)])
 def test_gemm_persistent_multi_tile(shape):
     """Grids with more tiles than resident workgroups: each workgroup walks several tiles with
     one LDS-DMA ring across tile boundaries (K = 64: every K-step ends a tile; N = 2098: the
@@ -104,6 +127,8 @@ def test_gemm_persistent_multi_tile(shape):
     try:
         for cfg in list(range(C.lib().clm_gemm_num_configs())) + [-1]:
             for epi in (C.CLM_EPI_STORE, C.CLM_EPI_RESID):
+                if not _g4_ok(cfg, epi, N, K, N):
+                    continue
                 outs = []
                 for dbg in (0, 4):
                     C.lib().clm_debug_set(dbg)
@@ -270,6 +295,8 @@ def test_epilogue_rounding_matches_torch(dtype, N):
     W = torch.zeros((N, K), dtype=td, device="cuda")
     want = bias.to(td).view(torch.int16).expand(M, N)
     for cfg in list(range(C.lib().clm_gemm_num_configs())) + [-1]:
+        if not _g4_ok(cfg, C.CLM_EPI_STORE, N, K, N):
+            continue
         out = torch.empty((M, N), dtype=td, device="cuda")
         _gemm(dtype, C.CLM_EPI_STORE, cfg, A, W, out, bias=bias)
         got = out.view(torch.int16)

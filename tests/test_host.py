@@ -159,7 +159,7 @@ def test_gemm_config_table_matches_the_test_matrix():
     """every tile config is reachable by the picker (k_gemm.hip pick_config); the GPU test matrix
     (test_gpu_kernels.py) covers exactly these ids"""
     from clip_lora_match_amd import _capi as C
-    assert C.lib().clm_gemm_num_configs() == 13
+    assert C.lib().clm_gemm_num_configs() == 15
 
 
 def _f16_down(v):

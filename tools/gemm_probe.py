@@ -17,11 +17,15 @@ B = 256
 SHAPES = {"v_qkv": (B * 50, 2304, 768, 0), "v_out": (B * 50, 768, 768, 2), "v_fc1": (B * 50, 3072, 768, 1),
           "v_fc2": (B * 50, 768, 3072, 2), "t_qkv": (B * 77, 1536, 512, 0), "t_out": (B * 77, 512, 512, 2),
           "t_fc1": (B * 77, 2048, 512, 1), "t_fc2": (B * 77, 512, 2048, 2), "sq4096": (4096, 4096, 4096, 0),
+          "sq8k": (8192, 8192, 8192, 0),
+          # configs[3] ViT-L/14@336 at batch 128 (M = 128 x 577)
+          "l_qkv": (128 * 577, 3072, 1024, 0), "l_out": (128 * 577, 1024, 1024, 2),
+          "l_fc1": (128 * 577, 4096, 1024, 1), "l_fc2": (128 * 577, 1024, 4096, 2),
           # the pruned last layer: B pooled rows
           "pv_out": (B, 768, 768, 2), "pv_fc1": (B, 3072, 768, 1), "pv_fc2": (B, 768, 3072, 2),
           "pt_out": (B, 512, 512, 2), "pt_fc1": (B, 2048, 512, 1), "pt_fc2": (B, 512, 2048, 2)}
 cfgs = [int(x) for x in sys.argv[1].split(",")] if len(sys.argv) > 1 else [-1]
-only = sys.argv[2].split(",") if len(sys.argv) > 2 else [k for k in SHAPES if k != "sq4096" and k[0] != "p"]
+only = sys.argv[2].split(",") if len(sys.argv) > 2 else [k for k in SHAPES if k[0] in "vt"]
 dev = torch.device("cuda", 0)
 L = C.lib()
 st = torch.cuda.current_stream()
