@@ -133,10 +133,22 @@ __device__ __forceinline__ void epi4_resid(const GemmArgs& g, const f32x4 (&acc)
   }
 }
 
+template <int N> struct IC4 { static constexpr int value = N; };
+
+// Main loop, per K-step (two 32-deep halves kk0 / kk1 of the two-buffer ring, G2's order):
+//   read kk1 fragments | 64 MFMAs on kk0 (fragments read one step earlier) | wait DMA + barrier |
+//   DMA of the K-step two ahead into the buffer just released | read the next kk0 fragments |
+//   64 MFMAs on kk1
+// At one wave per SIMD no other wave fills the MFMA pipe while a wave issues its 16 LDS-DMA pieces
+// (~60 cycles each among MFMAs), so the steady loop is kept branch-free -- the DMA target (this
+// tile's K-step kt + 2 or the next tile's kt + 2 - nk, zeros past the last tile) is a select of
+// descriptors, the tile's first K-step is peeled -- and sched_group_barrier interleaves the DMA
+// pieces and fragment reads one per MFMA. The accumulators are pinned to AGPRs once per K-step.
 template <bool BF, int EPI, int BN>
 __device__ __forceinline__ void gemm4_body(const GemmArgs& ga, int bid, int G) {
   using C = Cfg4<BN>;
   constexpr int BM = C::BM, TM = C::TM, TN = C::TN;
+  constexpr int NP = C::LA + C::LB;   // DMA pieces per wave and K-step
   GemmArgs g = ga;   // varlen: the device-resident row count (the grid was sized for ga.M)
   if (g.m_dev) g.M = __builtin_amdgcn_readfirstlane(*g.m_dev);
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
@@ -147,8 +159,7 @@ __device__ __forceinline__ void gemm4_body(const GemmArgs& ga, int bid, int G) {
   const TileWalk tw = tile_walk(ntn * ntm, bid, G);
   if (tw.count <= 0) return;
   const int n_my = tw.count;
-  const int nk = g.K / BK;
-  const int S = n_my * nk;
+  const int nk = g.K / BK;   // >= 2 (gemm4_supports)
 
   auto coords = [&](int i, int& m0, int& n0) {
     const int t = tw.first + i * tw.stride;
@@ -175,18 +186,22 @@ __device__ __forceinline__ void gemm4_body(const GemmArgs& ga, int bid, int G) {
   const uint32_t ch0 = (uint32_t)((pc ^ ((r8 >> 1) & 7)) << 4);
   const uint32_t ch1 = (uint32_t)((pc ^ ((4 + (r8 >> 1)) & 7)) << 4);
   const uint32_t la0 = r8 * lda2 + ch0, lw0 = r8 * ldw2 + ch0, dch = ch1 - ch0;
-  __amdgpu_buffer_rsrc_t ra, rw;
-  int ld_i = 0, ld_kt = 0;
-  auto point = [&](int i) {
-    int m0, n0;
-    coords(i, m0, n0);
-    ra = buf_rsrc(g.A + (int64_t)m0 * g.lda, min(BM, g.M - m0) * (int)lda2);
-    rw = buf_rsrc(g.W + (int64_t)n0 * g.ldw, min(BN, g.N - n0) * (int)ldw2);
+  // tile i's descriptors; past the last tile every record is out of range (the DMA writes zeros
+  // into a buffer no later step reads)
+  auto tile_rsrc = [&](int i, __amdgpu_buffer_rsrc_t& ra, __amdgpu_buffer_rsrc_t& rw) {
+    if (i < n_my) {
+      int m0, n0;
+      coords(i, m0, n0);
+      ra = buf_rsrc(g.A + (int64_t)m0 * g.lda, min(BM, g.M - m0) * (int)lda2);
+      rw = buf_rsrc(g.W + (int64_t)n0 * g.ldw, min(BN, g.N - n0) * (int)ldw2);
+    } else {
+      ra = buf_rsrc(g.A, 0);
+      rw = buf_rsrc(g.W, 0);
+    }
   };
-  point(0);
-  auto dma_next = [&](int buf) {
+  auto dma = [&](__amdgpu_buffer_rsrc_t ra, __amdgpu_buffer_rsrc_t rw, int ktgt, int buf) {
     uint8_t* base = smem + buf * C::STAGE_BYTES;
-    const int so = __builtin_amdgcn_readfirstlane(ld_kt * BK * 2);
+    const int so = __builtin_amdgcn_readfirstlane(ktgt * BK * 2);
 #pragma unroll
     for (int j = 0; j < C::LA; ++j)
       __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, (lds_ptr4_t)(base + (wid * C::LA + j) * 1024), 16,
@@ -197,10 +212,6 @@ __device__ __forceinline__ void gemm4_body(const GemmArgs& ga, int bid, int G) {
       __builtin_amdgcn_raw_ptr_buffer_load_lds(rw, (lds_ptr4_t)(base + BM * 128 + (wid * C::LB + j) * 1024), 16,
                                                (lw0 + (uint32_t)((wid * C::LB + j) & 1) * dch) + (uint32_t)((wid * C::LB + j) * 8) * ldw2,
                                                so, 0, 0);
-    if (++ld_kt == nk) {
-      ld_kt = 0;
-      if (++ld_i < n_my) point(ld_i);
-    }
   };
   auto read_frags = [&](const uint8_t* sa, int kk, u32x4 (&af)[TM], u32x4 (&bw)[TN]) {
     const int c = kk * 4 + (lane >> 4);
@@ -216,46 +227,70 @@ __device__ __forceinline__ void gemm4_body(const GemmArgs& ga, int bid, int G) {
     }
   };
   f32x4 acc[TM][TN];
-  // first == true: C = 0 (the tile's first half K-step), so no accumulator is ever zeroed by VALU
-  auto mma = [&](const u32x4 (&af)[TM], const u32x4 (&bw)[TN], bool first) {
+  auto mma = [&](const u32x4 (&af)[TM], const u32x4 (&bw)[TN], auto firstc) {
+    constexpr bool FIRST = decltype(firstc)::value != 0;   // C = 0: the tile's first half K-step
 #pragma unroll
     for (int mb = 0; mb < TM; ++mb)
 #pragma unroll
-      for (int nb = 0; nb < TN; ++nb) {
-        acc[mb][nb] = mfma16<BF>(bw[nb], af[mb], first ? f32x4{0.f, 0.f, 0.f, 0.f} : acc[mb][nb]);
-        asm volatile("" : "+a"(acc[mb][nb]));   // the accumulator stays in AGPRs
-      }
+      for (int nb = 0; nb < TN; ++nb)
+        acc[mb][nb] = mfma16<BF>(bw[nb], af[mb], FIRST ? f32x4{0.f, 0.f, 0.f, 0.f} : acc[mb][nb]);
+  };
+  auto pin = [&]() {   // the accumulators stay in AGPRs
+#pragma unroll
+    for (int mb = 0; mb < TM; ++mb)
+#pragma unroll
+      for (int nb = 0; nb < TN; ++nb) asm volatile("" : "+a"(acc[mb][nb]));
   };
 
-  dma_next(0);
-  if (S > 1) dma_next(1);
-  if (S >= 2) wait_vmcnt<C::LA + C::LB>();   // DMA(0) retired, DMA(1) in flight
-  else wait_vmcnt<0>();
+  __amdgpu_buffer_rsrc_t ra, rw, rna, rnw;   // this tile's and the next tile's descriptors
+  tile_rsrc(0, ra, rw);
+  tile_rsrc(1, rna, rnw);
+  dma(ra, rw, 0, 0);
+  dma(ra, rw, 1, 1);
+  wait_vmcnt<0>();
   lds_barrier();
   u32x4 a0[TM], b0[TN], a1[TM], b1[TN];
   read_frags(smem, 0, a0, b0);
 
   constexpr int E0 = EPI == EPI_RESID ? TM * TN : TM * TN / 2;   // stores of one tile's epilogue
   constexpr int E = E0 > 63 ? 63 : E0;
-  int s = 0, cur = 0;
+  int cur = 0;
+  // one K-step (kt of this tile; FIRST: kt == 0, which may leave the previous epilogue's stores in
+  // flight -- they are younger than the DMA waited for)
+  auto step = [&](int kt, auto firstc) {
+    constexpr bool FIRST = decltype(firstc)::value != 0;
+    read_frags(smem + cur * C::STAGE_BYTES, 1, a1, b1);
+    mma(a0, b0, firstc);
+#pragma unroll
+    for (int j = 0; j < TM + TN; ++j) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);   // 1 MFMA
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);   // 1 LDS read
+    }
+    if constexpr (FIRST) wait_vmcnt<E>();
+    else wait_vmcnt<0>();
+    lds_barrier();
+    const bool same = kt + 2 < nk;
+    dma(same ? ra : rna, same ? rw : rnw, same ? kt + 2 : kt + 2 - nk, cur);
+    cur ^= 1;
+    read_frags(smem + cur * C::STAGE_BYTES, 0, a0, b0);
+    mma(a1, b1, IC4<0>{});
+#pragma unroll
+    for (int j = 0; j < NP; ++j) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);   // 1 MFMA
+      __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);   // 1 VMEM (LDS-DMA piece)
+    }
+#pragma unroll
+    for (int j = 0; j < TM + TN; ++j) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);   // 1 MFMA
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);   // 1 LDS read
+    }
+    pin();
+  };
   for (int ti = 0; ti < n_my; ++ti) {
     int m0, n0;
     coords(ti, m0, n0);
-    for (int kt = 0; kt < nk; ++kt, ++s) {
-      read_frags(smem + cur * C::STAGE_BYTES, 1, a1, b1);
-      if (kt == 0) mma(a0, b0, true);
-      else mma(a0, b0, false);
-      const int nxt = cur ^ 1;
-      if (s + 1 < S) {
-        if (kt == 0 && ti > 0) wait_vmcnt<E>();
-        else wait_vmcnt<0>();
-        lds_barrier();
-        if (s + 2 < S) dma_next(cur);
-        read_frags(smem + nxt * C::STAGE_BYTES, 0, a0, b0);
-      }
-      mma(a1, b1, false);
-      cur = nxt;
-    }
+    step(0, IC4<1>{});
+    for (int kt = 1; kt < nk; ++kt) step(kt, IC4<0>{});
     if (g.debug & 1) {
 #pragma unroll
       for (int mb = 0; mb < TM; ++mb)
@@ -266,7 +301,11 @@ __device__ __forceinline__ void gemm4_body(const GemmArgs& ga, int bid, int G) {
     } else {
       epi4_store<BF, EPI, BN>(g, acc, m0, n0, wm, wn, lane);
     }
+    ra = rna;
+    rw = rnw;
+    tile_rsrc(ti + 2, rna, rnw);
   }
+  wait_vmcnt<0>();   // the zero-filling DMA past the last tile and the last stores
 }
 
 template <bool BF, int EPI, int BN>
@@ -309,7 +348,7 @@ hipError_t by_id4(int id, const GemmArgs& g, hipStream_t s) {
 }  // namespace
 
 bool gemm4_supports(int epi, const GemmArgs& g) {
-  if (g.K % BK || g.ksplit > 1 || (g.N % 4) || (g.ldo % 4)) return false;
+  if (g.K % BK || g.K < 2 * BK || g.ksplit > 1 || (g.N % 4) || (g.ldo % 4)) return false;
   if (epi == EPI_RESID) return true;
   return (epi == EPI_STORE || epi == EPI_GELU) && (g.N % 8) == 0 && (g.ldo % 8) == 0 && ((uintptr_t)g.out & 15) == 0;
 }

@@ -22,10 +22,11 @@ def _gemm(dtype, epi, cfg, A, W, out, bias=None, rs=None, cs=None):
 
 def _g4_ok(cfg, epi, N, K, ldo):
     """configs 13 / 14 (G4, k_gemm4.hip gemm4_supports): STORE / GELU with N, ldo multiples of 8,
-    RESID with multiples of 4, whole 64-deep K-steps; anything else is refused (CLM_E_HIP)"""
+    RESID with multiples of 4, whole 64-deep K-steps and at least two of them; anything else is
+    refused (CLM_E_HIP)"""
     if cfg < 13:
         return True
-    if K % 64 or N % 4 or ldo % 4:
+    if K % 64 or K < 128 or N % 4 or ldo % 4:
         return False
     if epi == C.CLM_EPI_RESID:
         return True
