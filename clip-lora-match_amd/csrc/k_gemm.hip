@@ -338,6 +338,11 @@ int pick_config(int epi, int M, int N) {
   // the search's filter GEMM (K = 512, no stores): G2's loop, 256 x 192 -- configs[4] search
   // 95.9 k QPS vs 86.4 k with gemm_kernel 256 x 256 (profiles/r04_v7_search_cfg_ab.txt)
   if (epi == EPI_FILTER) return pick_from(MODELS_G2, M, N);
+  // Large M x N plain stores (>= 4 full rounds of 256 x 256 tiles, e.g. ViT-L/14@336 batch 128: qkv
+  // 73,856 x 3,072): G4's one-wave-per-SIMD 256 x 256 tile (config 13), 439 vs 457 us for config 1
+  // with its stores (profiles/r06_v3_g4_probe.jsonl; $CLM_G4_STORE=0 keeps config 1)
+  static const int g4_store = getenv("CLM_G4_STORE") ? atoi(getenv("CLM_G4_STORE")) : 1;
+  if (epi == EPI_STORE && g4_store && (int64_t)((M + 255) / 256) * ((N + 255) / 256) >= 4 * 256) return 13;
   if (epi != EPI_GELU) return pick_from(MODELS, M, N);
   // Large M (>= 4 full rounds of 256 x 256 tiles, e.g. ViT-L/14@336 batch 128: fc1 73,856 x 4,096):
   // quantisation no longer favours G2's narrower tiles: gemm_kernel 256 x 256 takes 636 us there
