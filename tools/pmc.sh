@@ -15,7 +15,7 @@ for grp in "FETCH_SIZE" "WRITE_SIZE" "SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU_MFM
            "TCC_HIT_sum TCC_MISS_sum GRBM_GUI_ACTIVE"; do
   i=$((i+1))
   CLM_GEMM_CONCURRENT=1 timeout -k 10 240 rocprofv3 --kernel-trace --pmc $grp --output-format csv -d gpurun_out/pmc/p$i -o run -- \
-    python3 bench.py --steps 2 --warmup 1 --no-search --no-cpu-baseline --no-l14 --no-parity-mode --no-varlen --no-index-build --no-unmerged --sequential \
+    python3 bench.py --steps 2 --warmup 1 --no-search --no-cpu-baseline --no-l14 --no-parity-mode --no-varlen --no-index-build --no-unmerged --no-encode-item --sequential \
     > gpurun_out/pmc/p$i.log 2>&1
   rc=$?; echo "pmc pass $i ($grp) rc=$rc"
   [ $rc -eq 0 ] || { tail -5 gpurun_out/pmc/p$i.log; exit $rc; }
