@@ -1,8 +1,8 @@
 #!/bin/bash
-# scratch GPU session script (the command of the last gpurun call): the default bench line at HEAD with
-# its step trace kept, and a rocprofv3 --stats summary of the headline step
+# scratch GPU session script (the command of the last gpurun call): persistent fused q/k/v + attention
+# (next tile's first K-step and bias fetched under the attention): encode tests, then a same-session
+# A/B of the pair step (A = HEAD, B = persistent)
 cd "$(dirname "$0")/.." && export TMPDIR=/tmp && mkdir -p gpurun_out
-rm -rf gpurun_out/trace
-CLM_TRACE_KEEP=gpurun_out/trace timeout -k 10 900 python -u bench.py > gpurun_out/r06p_bench.json 2> gpurun_out/r06p_bench.err; rc=$?
-echo "bench rc=$rc"; tail -c 300 gpurun_out/r06p_bench.json; [ $rc -eq 0 ] || { tail -5 gpurun_out/r06p_bench.err; exit $rc; }
-ls gpurun_out/trace | head
+timeout -k 10 600 python -u -m pytest tests/test_gpu_encode.py tests/test_gpu_dropin.py -x -q --timeout 300 --timeout-method thread > gpurun_out/r06q_pytest.log 2>&1; rc=$?
+echo "pytest rc=$rc"; grep -E "FAIL|Error|passed|failed" gpurun_out/r06q_pytest.log | tail -5; [ $rc -eq 0 ] || exit $rc
+ARMS="A=A B=B" REPS=3 BENCH_ARGS="--no-trace --no-encode-item" bash tools/ab.sh
