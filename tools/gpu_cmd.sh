@@ -1,13 +1,10 @@
 #!/bin/bash
-# scratch GPU session script (the command of the last gpurun call): the default bench line three times on one
-# box (run-to-run spread of every leg)
+# scratch GPU session script (the command of the last gpurun call): fused residual + LayerNorm -- bit-identity
+# tests, then the pair-step A/B: A = fused (default), B = separate LayerNorm launches, C = LayerNorms skipped
+# (wrong embeddings, the upper bound of the LayerNorm launches' cost)
 cd "$(dirname "$0")/.." && export TMPDIR=/tmp && mkdir -p gpurun_out
-for r in 1 2 3; do
-  timeout -k 10 900 python -u bench.py --no-trace > gpurun_out/r06t_bench$r.json 2> gpurun_out/r06t_bench$r.err; rc=$?
-  echo "bench $r rc=$rc"; [ $rc -eq 0 ] || { tail -5 gpurun_out/r06t_bench$r.err; exit $rc; }
-  python3 -c "
-import json
-d=json.loads(open('gpurun_out/r06t_bench$r.json').read().strip().splitlines()[-1])
-print($r, d['value'], d['ms_per_step'], d['search']['qps'], d['l14']['images_per_s'], d['index_build']['images_per_s'], d['search']['single']['ms_per_query'])
-"
-done
+timeout -k 10 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_gpu_encode.py \
+  -k "fused_resid_layernorm or pair_streams or text_varlen or last_layer_pruning" > gpurun_out/r06w_tests.log 2>&1; rc=$?
+tail -15 gpurun_out/r06w_tests.log; [ $rc -eq 0 ] || exit $rc
+REPS=3 ARMS="A=cur B=cur:CLM_FUSED_LN=0 C=cur:CLM_FUSED_LN=0,CLM_SKIP_LN=1" \
+  BENCH_ARGS="--no-trace --no-single --no-encode-item --no-near-dup --no-persist" bash tools/ab.sh
