@@ -955,6 +955,12 @@ namespace {
 // (DMA + store) groups; the first and last D - 1 blocks, and the extra chunk-maximum stores, only
 // ever make the wait longer (vmcnt(0) there).
 constexpr int SCAN_CHUNK = 256;
+// cache policy of the index stream's LDS-DMA: nt (non-temporal; each row is read once per call):
+// single-query device time 1.763 -> 1.682 ms at 10 M x 512, 0.729 -> 0.764 of HBM, nq = 1..16 all
+// 4-6 % faster (profiles/r06_v15_scan16_nt_ab.txt)
+#ifndef CLM_SCAN_AUX
+#define CLM_SCAN_AUX 2
+#endif
 template <int KS, int D>
 __device__ __forceinline__ void scan16_body(const Scan16Args& a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
@@ -1029,8 +1035,8 @@ __device__ __forceinline__ void scan16_body(const Scan16Args& a) {
     uint8_t* base = ring + buf * BLK;
 #pragma unroll
     for (int t = 0; t < KS; ++t)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_ptr_t)(base + t * 1024), 16, doff[t], 0, 0, 0);
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(ri, (lds_ptr_t)(base + 16 * RB), 16, ioff, 0, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_ptr_t)(base + t * 1024), 16, doff[t], 0, 0, CLM_SCAN_AUX);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(ri, (lds_ptr_t)(base + 16 * RB), 16, ioff, 0, 0, CLM_SCAN_AUX);
   };
 #pragma unroll
   for (int j = 0; j < D - 1; ++j)

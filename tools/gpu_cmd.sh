@@ -1,17 +1,18 @@
 #!/bin/bash
-# scratch GPU session script (the command of the last gpurun call): fused residual + LayerNorm on single-stream
-# launches -- bit-identity tests, then the pair step + L/14 leg A/B: A = default (fused on single-stream
-# encodes: the L/14 leg), B = $CLM_FUSED_LN=0 (separate LayerNorm launches everywhere)
+# scratch GPU session script (the command of the last gpurun call): single-query scan (scan16) with the
+# non-temporal (nt) cache policy on its LDS-DMA index stream: A = HEAD, NT = k_search.hip built with
+# -DCLM_SCAN_AUX=2; search + single-query legs, 3 rounds alternating
 cd "$(dirname "$0")/.." && export TMPDIR=/tmp && mkdir -p gpurun_out/ab
-timeout -k 10 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_gpu_encode.py \
-  -k "fused_resid_layernorm or pair_streams or text_varlen or last_layer_pruning or l14" > gpurun_out/r06x_tests.log 2>&1; rc=$?
-tail -12 gpurun_out/r06x_tests.log; [ $rc -eq 0 ] || exit $rc
+cp clip-lora-match_amd/libclm.so ab/libclm_cur.so
 for rep in 1 2 3; do
-  for arm in A B; do
-    envs=""; [ $arm = B ] && envs="CLM_FUSED_LN=0"
-    env $envs timeout -k 10 300 python bench.py --no-search --no-cpu-baseline --no-varlen --no-index-build --no-unmerged \
-      --no-parity-mode --no-trace --no-single --no-encode-item --no-near-dup --no-persist > gpurun_out/ab/l$arm.$rep.json 2> gpurun_out/ab/l$arm.$rep.err
-    rc=$?; [ $rc -eq 0 ] || { tail -5 gpurun_out/ab/l$arm.$rep.err; exit $rc; }
-    python -c "import json; d=json.load(open('gpurun_out/ab/l$arm.$rep.json')); print('$arm', $rep, d['value'], d['ms_per_step'], d['l14']['images_per_s'], d['l14'].get('ms_per_step'))"
+  for arm in A NT; do
+    cp ab/libclm_$arm.so clip-lora-match_amd/libclm.so
+    timeout -k 10 400 python bench.py --no-cpu-baseline --no-l14 --no-varlen --no-index-build --no-unmerged --no-parity-mode \
+      --no-trace --no-encode-item --no-near-dup --no-persist > gpurun_out/ab/s$arm.$rep.json 2> gpurun_out/ab/s$arm.$rep.err
+    rc=$?; [ $rc -eq 0 ] || { tail -5 gpurun_out/ab/s$arm.$rep.err; cp ab/libclm_cur.so clip-lora-match_amd/libclm.so; exit $rc; }
+    python -c "
+import json; d=json.load(open('gpurun_out/ab/s$arm.$rep.json')); s=d['search']; t=s['single']
+print('$arm', $rep, d['value'], s['qps'], t['ms_per_query'], t['device_ms_per_query'], t['device_hbm_frac'], [t['per_call_batch'][k]['ms_per_call'] for k in ('1','2','4','8','16')], t['equal_to_exact_scan'])"
   done
 done
+cp ab/libclm_cur.so clip-lora-match_amd/libclm.so
