@@ -1,17 +1,15 @@
 #!/bin/bash
-# scratch GPU session script (the command of the last gpurun call): batched search with the nt cache policy on the
-# filter GEMM's index-row DMA (A = HEAD, NT = k_gemm2.hip built with -DCLM_FILTER_W_AUX=2); search legs, 3 rounds
+# scratch GPU session script (the command of the last gpurun call): single-query scan shape with the nt policy:
+# waves per CU x ring depth (A = 1 x 4, the default; B = 2 x 4; C = 2 x 2; D = 4 x 2); search legs, 2 rounds
 cd "$(dirname "$0")/.." && export TMPDIR=/tmp && mkdir -p gpurun_out/ab
-cp clip-lora-match_amd/libclm.so ab/libclm_cur.so
-for rep in 1 2 3; do
-  for arm in A NT; do
-    cp ab/libclm_$arm.so clip-lora-match_amd/libclm.so
-    timeout -k 10 400 python bench.py --no-cpu-baseline --no-l14 --no-varlen --no-index-build --no-unmerged --no-parity-mode \
-      --no-trace --no-encode-item --no-single --no-persist > gpurun_out/ab/f$arm.$rep.json 2> gpurun_out/ab/f$arm.$rep.err
-    rc=$?; [ $rc -eq 0 ] || { tail -5 gpurun_out/ab/f$arm.$rep.err; cp ab/libclm_cur.so clip-lora-match_amd/libclm.so; exit $rc; }
+for rep in 1 2; do
+  for arm in A B C D; do
+    case $arm in A) envs="";; B) envs="CLM_SCAN_NW=2 CLM_SCAN_D=4";; C) envs="CLM_SCAN_NW=2 CLM_SCAN_D=2";; D) envs="CLM_SCAN_NW=4 CLM_SCAN_D=2";; esac
+    env $envs timeout -k 10 400 python bench.py --no-cpu-baseline --no-l14 --no-varlen --no-index-build --no-unmerged --no-parity-mode \
+      --no-trace --no-encode-item --no-near-dup --no-persist > gpurun_out/ab/w$arm.$rep.json 2> gpurun_out/ab/w$arm.$rep.err
+    rc=$?; [ $rc -eq 0 ] || { tail -5 gpurun_out/ab/w$arm.$rep.err; exit $rc; }
     python -c "
-import json; d=json.load(open('gpurun_out/ab/f$arm.$rep.json')); s=d['search']
-print('$arm', $rep, d['value'], s['qps'], s['tflops'], s['check']['match'], s.get('near_dup', {}).get('qps'))"
+import json; d=json.load(open('gpurun_out/ab/w$arm.$rep.json')); t=d['search']['single']
+print('$arm', $rep, t['ms_per_query'], t['device_ms_per_query'], t['device_hbm_frac'], [t['per_call_batch'][k]['ms_per_call'] for k in ('1','2','4','8','16')], t['equal_to_exact_scan'])"
   done
 done
-cp ab/libclm_cur.so clip-lora-match_amd/libclm.so
